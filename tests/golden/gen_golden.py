@@ -1,0 +1,426 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REAL reference (read-only, this container only).
+
+    PYTHONPATH=/root/reference python3 -B tests/golden/gen_golden.py
+
+The reference (ThorLL/Element-Crush-Gym) ships no tests or fixtures of its own
+(SURVEY.md §4), so these vectors are the parity anchor: every array in
+``tests/golden/*.npz`` is produced by calling the reference's own functions
+(``match3tile.boardv2.BoardV2``, ``match3tile.boardFunctions``, numpy's legacy
+``RandomState``). Only data is committed -- no reference source.
+
+Files written:
+  prng.npz        MT19937 raw streams, randint/random_interval/shuffle/choice chains
+  matches.npz     get_matches mask + get_match_spawn_mask on crafted + random token boards
+  legal.npz       legal_actions bitmasks on play boards, boards with specials, dead boards
+  init.npz        BoardV2.__init__ boards + raw draws consumed (9x9x6, 16x16x8)
+  steps.npz       apply_action transitions (board, seed, n_actions, action) -> (board', reward, draws)
+                  incl. specials, all combo pairs, typed specials, illegal swaps, terminal boards
+  episodes.npz    samplerTasks.random_task-style seeded episodes (actions, rewards, draws, final board)
+  shuffle.npz     dead-board transitions that terminate (shuffle path) + seeds that cycle forever
+"""
+from __future__ import annotations
+
+import os
+import signal
+import sys
+from multiprocessing import Pool
+
+sys.dont_write_bytecode = True
+REF = os.environ.get("M3_REFERENCE", "/root/reference")
+if REF not in sys.path:
+    sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+
+from match3tile.boardConfig import BoardConfig  # noqa: E402
+from match3tile.boardFunctions import get_matches, get_match_spawn_mask, legal_actions  # noqa: E402
+from match3tile.boardv2 import BoardV2  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+SHAPES = [(9, 9, 6), (16, 16, 8)]
+
+
+def raw(n):
+    return np.random.mtrand._rand._bit_generator.random_raw(n).astype(np.uint32)
+
+
+def draws_since_seed(seed: int) -> int:
+    """Raw MT outputs consumed since np.random.seed(seed), read off numpy's global state."""
+    st = np.random.get_state()
+    key, pos = st[1], st[2]
+    fresh = np.random.RandomState(seed).get_state()
+    if pos == 624 and np.array_equal(fresh[1], key):
+        return 0
+    for t in range(1, 16):
+        d = (t - 1) * 624 + pos
+        rs = np.random.RandomState(seed)
+        rs._bit_generator.random_raw(d)
+        s2 = rs.get_state()
+        if s2[2] == pos and np.array_equal(s2[1], key):
+            return d
+    raise RuntimeError("could not determine draw count")
+
+
+def legal_bits(cfg, arr):
+    bits = np.zeros(cfg.action_space, dtype=np.uint8)
+    for a in legal_actions(cfg, arr):
+        bits[a] = 1
+    return bits
+
+
+# ------------------------------------------------------------------------- PRNG
+def gen_prng():
+    seeds = np.array([1, 100, 12345, 2**31 - 2, 2**32 - 1, 0, 7, 424242], dtype=np.uint64)
+    raw_streams = []
+    for s in seeds:
+        np.random.seed(int(s))
+        raw_streams.append(raw(1500))
+    # randint chains with size (the reference's tile refill / init calls)
+    chains = {}
+    for hi in (7, 9):
+        out = []
+        for s in seeds:
+            np.random.seed(int(s))
+            out.append(np.random.randint(1, hi, size=300))
+        chains[f"randint_1_{hi}"] = np.array(out, dtype=np.int64)
+    # choice over lists of every length 1..200 (random_action contract, samplerTasks.py:13)
+    ch = []
+    for n in range(1, 201):
+        np.random.seed(n * 7919)
+        lst = list(range(1000, 1000 + n))
+        ch.append([np.random.choice(lst) for _ in range(8)])
+    # legacy shuffle of rows (boardFunctions.py:22)
+    perms = []
+    for R in (9, 16):
+        for s in seeds:
+            np.random.seed(int(s))
+            a = np.arange(R * 3).reshape(R, 3)
+            np.random.shuffle(a)
+            perms.append(np.concatenate([a[:, 0] // 3, np.full(16 - R, -1)]))
+    np.savez_compressed(os.path.join(OUT, "prng.npz"), seeds=seeds, raw=np.array(raw_streams),
+                        choice=np.array(ch, dtype=np.int64), shuffle_rows=np.array(perms, dtype=np.int64),
+                        **chains)
+
+
+# ---------------------------------------------------------------------- matches
+def crafted_token_boards(R, C, T, rng):
+    boards = []
+    z = lambda: rng.integers(1, T + 1, size=(R, C))  # noqa: E731
+    # random boards have some runs; add a bunch of crafted shapes on top
+    for _ in range(300):
+        boards.append(z())
+    shapes = []
+    # L corner (horizontal arm starting at the corner), T, corner-both, line 4/5 h and v, cross, long lines
+    shapes.append([(0, 0), (1, 0), (2, 0), (2, 1), (2, 2)])
+    shapes.append([(0, 0), (0, 1), (0, 2), (1, 0), (2, 0)])
+    shapes.append([(0, 1), (1, 1), (2, 1), (2, 0), (2, 2)])
+    shapes.append([(1, 0), (1, 1), (1, 2), (0, 1), (2, 1)])
+    shapes.append([(0, 0), (0, 1), (0, 2), (0, 3)])
+    shapes.append([(0, 0), (0, 1), (0, 2), (0, 3), (0, 4)])
+    shapes.append([(0, 0), (1, 0), (2, 0), (3, 0)])
+    shapes.append([(0, 0), (1, 0), (2, 0), (3, 0), (4, 0)])
+    shapes.append([(0, 2), (1, 2), (2, 2), (2, 0), (2, 1), (2, 3), (2, 4), (3, 2), (4, 2)])
+    shapes.append([(0, 3), (1, 3), (2, 3), (2, 1), (2, 2), (3, 1), (4, 1), (2, 4)])
+    shapes.append([(0, 0), (0, 1), (0, 2), (1, 2), (2, 2), (2, 3), (2, 4), (3, 4), (4, 4)])
+    shapes.append([(r, 4) for r in range(7)])
+    shapes.append([(4, c) for c in range(8)])
+    for shp in shapes:
+        for _ in range(12):
+            b = z()
+            orr, oc = rng.integers(0, 4), rng.integers(0, 4)
+            v = rng.integers(1, T + 1)
+            for (r, c) in shp:
+                rr, cc = min(r + orr, R - 1), min(c + oc, C - 1)
+                b[rr, cc] = v
+            # sprinkle zeros (removed cells) sometimes
+            if rng.random() < 0.3:
+                b[rng.integers(0, R), rng.integers(0, C)] = 0
+            boards.append(b)
+    # few-type boards produce many/large merged groups
+    for _ in range(150):
+        boards.append(rng.integers(1, min(T, 3) + 1, size=(R, C)))
+    for _ in range(60):
+        b = rng.integers(1, 3, size=(R, C))
+        b[rng.random((R, C)) < 0.15] = 0
+        boards.append(b)
+    return boards
+
+
+def gen_matches():
+    rng = np.random.default_rng(1234)
+    out = {}
+    for (R, C, T) in SHAPES:
+        cfg = BoardConfig(seed=1, rows=R, columns=C, types=T)
+        tbs, masks, spawns, ngroups = [], [], [], []
+        for b in crafted_token_boards(R, C, T, rng):
+            b = np.asarray(b, dtype=np.int64)
+            mask, matches = get_matches(b.copy())
+            spawn = get_match_spawn_mask(cfg, [list(m) for m in matches])
+            tbs.append(b)
+            masks.append(mask)
+            spawns.append(spawn)
+            ngroups.append(len(matches))
+        tag = f"{R}x{C}x{T}"
+        out[f"tb_{tag}"] = np.array(tbs, dtype=np.int8)
+        out[f"mask_{tag}"] = np.array(masks, dtype=np.uint8)
+        out[f"spawn_{tag}"] = np.array(spawns, dtype=np.int32)
+        out[f"ngroups_{tag}"] = np.array(ngroups, dtype=np.int32)
+    np.savez_compressed(os.path.join(OUT, "matches.npz"), **out)
+
+
+# ------------------------------------------------------------------------ init
+def _init_one(args):
+    R, C, T, seed = args
+    cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
+    b = BoardV2(20, cfg)
+    return b.array.astype(np.int8), draws_since_seed(int(seed))
+
+
+def gen_init(pool):
+    out = {}
+    for (R, C, T), n in zip(SHAPES, (1024, 256)):
+        seeds = np.concatenate([np.arange(1, n - 3), [2**31 - 2, 2**32 - 1, 123456789, 987654321]]).astype(np.uint64)
+        res = pool.map(_init_one, [(R, C, T, s) for s in seeds])
+        tag = f"{R}x{C}x{T}"
+        out[f"seeds_{tag}"] = seeds
+        out[f"boards_{tag}"] = np.array([r[0] for r in res])
+        out[f"draws_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+    np.savez_compressed(os.path.join(OUT, "init.npz"), **out)
+
+
+# ---------------------------------------------------------------------- episodes
+def _episode(args):
+    """samplerTasks.random_task (samplerTasks.py:9-14) with a fixed seed."""
+    R, C, T, seed, moves = args
+    cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
+    state = BoardV2(moves, cfg)
+    init_board = state.array.astype(np.int8)
+    np.random.seed(cfg.seed)
+    acts, rews, drws, boards = [], [], [], []
+    prev = 0
+    while not state.is_terminal:
+        a = int(np.random.choice(state.legal_actions))
+        state = state.apply_action(a)
+        acts.append(a)
+        rews.append(int(state.reward - prev))
+        prev = state.reward
+        drws.append(draws_since_seed(int(seed)))
+        boards.append(state.array.astype(np.int8))
+    return init_board, acts, rews, drws, boards
+
+
+def gen_episodes(pool):
+    out = {}
+    for (R, C, T), n in zip(SHAPES, (1024, 192)):
+        seeds = np.arange(1, n + 1, dtype=np.uint64)
+        res = pool.map(_episode, [(R, C, T, s, 20) for s in seeds], chunksize=4)
+        tag = f"{R}x{C}x{T}"
+        out[f"seeds_{tag}"] = seeds
+        out[f"init_{tag}"] = np.array([r[0] for r in res])
+        out[f"actions_{tag}"] = np.array([r[1] for r in res], dtype=np.int16)
+        out[f"rewards_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+        out[f"draws_{tag}"] = np.array([r[3] for r in res], dtype=np.int16)
+        # every board of the first 128 episodes, final board for all
+        bs = np.array([r[4] for r in res])
+        out[f"boards_{tag}"] = bs[:128]
+        out[f"final_{tag}"] = bs[:, -1]
+    np.savez_compressed(os.path.join(OUT, "episodes.npz"), **out)
+
+
+# ------------------------------------------------------------------------- steps
+def _step_case(args):
+    R, C, T, board, seed, n_actions, action = args
+    cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
+    st = BoardV2(int(n_actions), cfg, np.array(board, dtype=np.int64))
+    np.random.seed(999)  # apply_action must reseed; a terminal board must not touch the RNG
+    before = np.random.get_state()
+    nxt = st.apply_action(int(action))
+    if st.is_terminal:
+        after = np.random.get_state()
+        assert after[2] == before[2] and np.array_equal(after[1], before[1])
+        d = -1
+    else:
+        d = draws_since_seed(int(seed))
+    return nxt.array.astype(np.int8), int(nxt.reward), d, int(nxt.n_actions)
+
+
+def step_cases(R, C, T, rng, n_play=1500):
+    cfg = BoardConfig(seed=1, rows=R, columns=C, types=T)
+    H, V, B, M, TM = cfg.h_line, cfg.v_line, cfg.bomb, cfg.mega_token, cfg.type_mask
+    specials = [H, V, B, M]
+    cases = []
+    # boards from seeded play
+    play = []
+    for s in range(1, 120):
+        c2 = BoardConfig(seed=s, rows=R, columns=C, types=T)
+        b = BoardV2(20, c2)
+        np.random.seed(s)
+        for _ in range(6):
+            play.append((b.array.copy(), s))
+            la = b.legal_actions
+            b = b.apply_action(int(np.random.choice(la)))
+    for i in range(n_play):
+        board, s = play[rng.integers(0, len(play))]
+        board = board.copy()
+        kind = rng.random()
+        if kind < 0.35:
+            for _ in range(rng.integers(1, 4)):       # sprinkle pure specials
+                board[rng.integers(0, R), rng.integers(0, C)] = specials[rng.integers(0, 4)]
+        elif kind < 0.45:                              # typed specials (dataset.type_switch style)
+            for _ in range(rng.integers(1, 3)):
+                r, c = rng.integers(0, R), rng.integers(0, C)
+                board[r, c] = min(127, int(board[r, c] & TM) + specials[rng.integers(0, 3)])
+        if rng.random() < 0.6:
+            la = legal_actions(cfg, board)
+            a = int(la[rng.integers(0, len(la))]) if la else int(rng.integers(0, cfg.action_space))
+        else:
+            a = int(rng.integers(0, cfg.action_space))
+        seed = int(rng.integers(1, 2**32))
+        cases.append((board, seed, 20, a))
+    # every combo pair at interior and edge positions
+    for sa in specials + [1]:
+        for sb in specials + [1]:
+            for _ in range(14):
+                board, _ = play[rng.integers(0, len(play))]
+                board = board.copy()
+                a = int(rng.integers(0, cfg.action_space))
+                (r1, c1), (r2, c2) = cfg.decode(a)
+                board[r1, c1], board[r2, c2] = sa, sb
+                cases.append((board, int(rng.integers(1, 2**32)), 20, a))
+    # bombs / lines at every edge cell (transposed-window quirk)
+    for r in range(R):
+        for c in (0, 1, C - 1):
+            board, _ = play[rng.integers(0, len(play))]
+            board = board.copy()
+            board[r, c] = specials[rng.integers(0, 4)]
+            cases.append((board, int(rng.integers(1, 2**32)), 20, int(rng.integers(0, cfg.action_space))))
+    # large typed values (dataset type_switch produces up to M + STM)
+    for _ in range(40):
+        board, _ = play[rng.integers(0, len(play))]
+        board = board.copy()
+        for _ in range(3):
+            board[rng.integers(0, R), rng.integers(0, C)] = int(rng.integers(TM + 1, 128))
+        cases.append((board, int(rng.integers(1, 2**32)), 20, int(rng.integers(0, cfg.action_space))))
+    # terminal boards (n_actions < 1) and n_actions == 1
+    for na in (0, -3, 1):
+        board, s = play[rng.integers(0, len(play))]
+        cases.append((board.copy(), s, na, int(rng.integers(0, cfg.action_space))))
+    return cases
+
+
+def gen_steps(pool):
+    rng = np.random.default_rng(4321)
+    out = {}
+    for (R, C, T), n in zip(SHAPES, (3000, 800)):
+        cases = step_cases(R, C, T, rng, n)
+        res = pool.map(_step_case, [(R, C, T, b, s, na, a) for (b, s, na, a) in cases], chunksize=16)
+        tag = f"{R}x{C}x{T}"
+        out[f"board_{tag}"] = np.array([c[0] for c in cases], dtype=np.int8)
+        out[f"seed_{tag}"] = np.array([c[1] for c in cases], dtype=np.uint32)
+        out[f"n_actions_{tag}"] = np.array([c[2] for c in cases], dtype=np.int32)
+        out[f"action_{tag}"] = np.array([c[3] for c in cases], dtype=np.int32)
+        out[f"next_{tag}"] = np.array([r[0] for r in res])
+        out[f"reward_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        out[f"draws_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+    np.savez_compressed(os.path.join(OUT, "steps.npz"), **out)
+
+
+# ------------------------------------------------------------------------- legal
+def gen_legal():
+    rng = np.random.default_rng(99)
+    out = {}
+    for (R, C, T) in SHAPES:
+        cfg = BoardConfig(seed=1, rows=R, columns=C, types=T)
+        boards = []
+        for s in range(1, 200):
+            c2 = BoardConfig(seed=s, rows=R, columns=C, types=T)
+            boards.append(BoardV2(20, c2).array.copy())
+        for _ in range(300):
+            b = rng.integers(1, T + 1, size=(R, C))
+            if rng.random() < 0.5:
+                for _ in range(rng.integers(1, 5)):
+                    b[rng.integers(0, R), rng.integers(0, C)] = [cfg.h_line, cfg.v_line, cfg.bomb,
+                                                                  cfg.mega_token, 0][rng.integers(0, 5)]
+            boards.append(b)
+        for m in range(2, T + 1):   # dead-ish patterned boards
+            for a in range(1, 4):
+                for bb in range(1, 4):
+                    boards.append(np.fromfunction(lambda r, c: (a * r + bb * c) % m + 1, (R, C), dtype=np.int64))
+        tag = f"{R}x{C}x{T}"
+        out[f"boards_{tag}"] = np.array(boards, dtype=np.int8)
+        out[f"legal_{tag}"] = np.array([legal_bits(cfg, b) for b in boards], dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "legal.npz"), **out)
+
+
+# ----------------------------------------------------------------------- shuffle
+class _Timeout(Exception):
+    pass
+
+
+def _alarm(signum, frame):
+    raise _Timeout()
+
+
+def _shuffle_case(args):
+    R, C, T, board, seed, action = args
+    cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
+    signal.signal(signal.SIGALRM, _alarm)
+    signal.alarm(3)
+    try:
+        nxt = BoardV2(20, cfg, np.array(board, dtype=np.int64)).apply_action(int(action))
+        signal.alarm(0)
+        return nxt.array.astype(np.int8), int(nxt.reward), draws_since_seed(int(seed)), 1
+    except _Timeout:
+        return np.zeros((R, C), np.int8), 0, 0, 0
+
+
+def gen_shuffle(pool):
+    """Boards whose post-swap cascade ends dead: exercise the shuffle loop (boardv2.py:188-194)."""
+    out = {}
+    for (R, C, T) in SHAPES:
+        cfg = BoardConfig(seed=1, rows=R, columns=C, types=T)
+        cases = []
+        for m in range(2, T + 1):
+            for a in range(1, 5):
+                for bb in range(1, 5):
+                    board = np.fromfunction(lambda r, c: (a * r + bb * c) % m + 1, (R, C), dtype=np.int64)
+                    # a swap of two cells inside one row keeps most of the pattern dead
+                    for seed in (1, 2, 3, 17, 12345):
+                        for act in (0, C - 1, 2 * C):
+                            cases.append((board, seed, act))
+        res = pool.map(_shuffle_case, [(R, C, T, b, s, a) for (b, s, a) in cases], chunksize=8)
+        tag = f"{R}x{C}x{T}"
+        out[f"board_{tag}"] = np.array([c[0] for c in cases], dtype=np.int8)
+        out[f"seed_{tag}"] = np.array([c[1] for c in cases], dtype=np.uint32)
+        out[f"action_{tag}"] = np.array([c[2] for c in cases], dtype=np.int32)
+        out[f"next_{tag}"] = np.array([r[0] for r in res])
+        out[f"reward_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        out[f"draws_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+        out[f"terminates_{tag}"] = np.array([r[3] for r in res], dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "shuffle.npz"), **out)
+
+
+def main():
+    which = sys.argv[1:] or ["prng", "matches", "legal", "init", "steps", "episodes", "shuffle"]
+    with Pool(8) as pool:
+        for w in which:
+            print("generating", w, flush=True)
+            if w == "prng":
+                gen_prng()
+            elif w == "matches":
+                gen_matches()
+            elif w == "legal":
+                gen_legal()
+            elif w == "init":
+                gen_init(pool)
+            elif w == "steps":
+                gen_steps(pool)
+            elif w == "episodes":
+                gen_episodes(pool)
+            elif w == "shuffle":
+                gen_shuffle(pool)
+
+
+if __name__ == "__main__":
+    main()
