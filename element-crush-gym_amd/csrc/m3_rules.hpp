@@ -1,0 +1,755 @@
+// m3_rules.hpp -- the env step of ThorLL/Element-Crush-Gym as bitboard code.
+//
+// One board per lane. A board is NP=7 bit-planes (cell values are int8 in
+// [0, 127]; plane p holds bit p of every cell), each plane a W-word bitboard
+// in registers. Everything the reference does cell-by-cell in Python/numpy is
+// restated as whole-board word operations:
+//   * TB = board & TM is planes [0, BITS); "TB == TB[x+d]" for every cell is
+//     one XOR/OR pass over BITS planes (eq<d>);
+//   * legal_actions (boardFunctions.py:26-112) is ~25 such comparisons;
+//   * get_matches (boardFunctions.py:121-156) is a sequential scan whose
+//     result depends on scan order; it is reproduced exactly by visiting only
+//     the run starts (cells that begin a horizontal or vertical triple) in
+//     ascending bit order and flood-filling runs with doubling shifts;
+//   * gravity (boardv2.py:166-173) is a few whole-board "drop everything
+//     above a hole by one row" passes;
+//   * scoring / merge / clip (boardv2.py:157-163) are popcounts and masks.
+// Cross-references to the reference are file:line in each function.
+#pragma once
+
+#include "m3_bitboard.hpp"
+#include "m3_rng.hpp"
+
+namespace m3 {
+
+constexpr int ceil_log2(int v) {
+    int b = 0;
+    while ((1 << b) < v) ++b;
+    return b;
+}
+
+// Flags, mirrored in include/m3.h.
+enum : uint32_t {
+    FLAG_TERMINAL = 0x01u,     // n_actions < 1: board returned unchanged (boardv2.py:44-45)
+    FLAG_BAD_ACTION = 0x02u,   // action id outside [0, A) (KeyError at boardv2.py:48)
+    FLAG_SHUFFLE_CAP = 0x04u,  // dead-board shuffle did not terminate within the cap (reference hangs)
+    FLAG_NO_LEGAL = 0x08u,     // no legal action to sample (np.random.choice([]) raises)
+    FLAG_SHUFFLED = 0x10u,     // the dead-board shuffle ran at least once
+    FLAG_RNG_OVERFLOW = 0x20u, // internal: step needed >= 624 draws; recomputed with FullMT
+};
+
+// BoardConfig (match3tile/boardConfig.py:26-43) as compile-time constants.
+template <int R_, int C_, int T_>
+struct Cfg {
+    static constexpr int R = R_, C = C_, T = T_;
+    static constexpr int N = R * C;
+    static constexpr int W = (N + 31) / 32;
+    static constexpr int BITS = ceil_log2(T + 1);
+    static constexpr int TM = (1 << BITS) - 1;
+    static constexpr int STM = (1 << (BITS + 1)) + 1 + TM;
+    static constexpr int H = TM + 1;
+    static constexpr int V = 2 * H;
+    static constexpr int B = STM;
+    static constexpr int M = TM + STM + 1;
+    static constexpr int A = R * (C - 1) * 2;
+    static constexpr int AW = (A + 31) / 32;
+    static constexpr int NP = 7;                 // value planes for int8 cells in [0, 127]
+    static constexpr int MAXG = N / 3 + 1;       // run-disjoint group creators, >= 3 cells each
+    static constexpr int SHUFFLE_CAP = 1024;
+    static_assert(R >= 4 && C >= 4 && R <= 16 && C <= 16, "board size");
+    static_assert(T >= 1 && BITS <= 4, "tile types must fit 4 bits");
+    using Bd = BB<W>;
+    using G = Geo<R, C, W>;
+};
+
+// --------------------------------------------------------------------------
+// small helpers
+// --------------------------------------------------------------------------
+template <class CF>
+M3_HD typename CF::Bd tb_nonzero(const typename CF::Bd* P) {
+    typename CF::Bd r = P[0];
+#pragma unroll
+    for (int p = 1; p < CF::BITS; ++p) r |= P[p];
+    return r;
+}
+
+template <class CF, int NPU>
+M3_HD typename CF::Bd special_mask(const typename CF::Bd* P) {  // board > TM
+    typename CF::Bd r = P[CF::BITS];
+#pragma unroll
+    for (int p = CF::BITS + 1; p < NPU; ++p) r |= P[p];
+    return r;
+}
+
+// bit y set iff TB[y] != TB[y + D]
+template <class CF, int D>
+M3_HD typename CF::Bd tb_ne(const typename CF::Bd* P) {
+    typename CF::Bd r = P[0] ^ at<D>(P[0]);
+#pragma unroll
+    for (int p = 1; p < CF::BITS; ++p) r |= P[p] ^ at<D>(P[p]);
+    return r;
+}
+template <class CF, int D>
+M3_HD typename CF::Bd tb_eq(const typename CF::Bd* P) {
+    return ~tb_ne<CF, D>(P);
+}
+
+template <class CF, int NPU>
+M3_HD int cell_value(const typename CF::Bd* P, int x) {
+    const int q = x >> 5, s = x & 31;
+    int v = 0;
+#pragma unroll
+    for (int p = 0; p < NPU; ++p) v |= (int)((P[p].word_at(q) >> s) & 1u) << p;
+    return v;
+}
+
+// write value v (< 2^NPU) into cell x, overwriting
+template <class CF, int NPU>
+M3_HD void set_cell(typename CF::Bd* P, int x, int v) {
+    const typename CF::Bd bm = CF::Bd::bit_at(x);
+#pragma unroll
+    for (int p = 0; p < NPU; ++p) {
+        const uint32_t on = 0u - (uint32_t)((v >> p) & 1);
+#pragma unroll
+        for (int i = 0; i < CF::W; ++i) P[p].w[i] = (P[p].w[i] & ~bm.w[i]) | (bm.w[i] & on);
+    }
+}
+
+// compile-time extraction of LEN (<= 32) bits starting at bit POS
+template <int POS, int LEN, int W>
+M3_HD uint32_t extract_bits(const BB<W>& b) {
+    constexpr int q = POS >> 5, s = POS & 31;
+    uint32_t lo = b.w[q] >> s;
+    if constexpr (s != 0 && q + 1 < W) lo |= b.w[q + 1] << (32 - s);
+    return LEN >= 32 ? lo : (lo & ((1u << (LEN & 31)) - 1u));
+}
+
+// --------------------------------------------------------------------------
+// legal_actions (boardFunctions.py:26-112), all 2*R*(C-1) candidates at once.
+// HL bit x: horizontal swap (x, x+1) is legal; VL bit x: vertical swap (x, x+C).
+// --------------------------------------------------------------------------
+template <class CF>
+M3_HD void legal_masks(const typename CF::Bd* P, const typename CF::Bd& spec,
+                       typename CF::Bd& HL, typename CF::Bd& VL) {
+    using Bd = typename CF::Bd;
+    using G = typename CF::G;
+    constexpr int C = CF::C, R = CF::R;
+    constexpr Bd VALID = G::valid();
+    const Bd z0 = VALID.andnot(tb_nonzero<CF>(P));  // TB == 0
+
+    // equalities shared by both directions
+    const Bd e1 = tb_eq<CF, 1>(P), e2 = tb_eq<CF, 2>(P), e3 = tb_eq<CF, 3>(P);
+    const Bd ecm1 = tb_eq<CF, C - 1>(P), ecp1 = tb_eq<CF, C + 1>(P);
+    const Bd e2cm1 = tb_eq<CF, 2 * C - 1>(P), e2cp1 = tb_eq<CF, 2 * C + 1>(P);
+    const Bd ec = tb_eq<CF, C>(P), e2c = tb_eq<CF, 2 * C>(P), e3c = tb_eq<CF, 3 * C>(P);
+    const Bd ecm2 = tb_eq<CF, C - 2>(P), ecp2 = tb_eq<CF, C + 2>(P);
+
+    constexpr Bd RGE1 = G::row_ge(1), RGE2 = G::row_ge(2), RLE2 = G::row_le(R - 2), RLE3 = G::row_le(R - 3);
+    constexpr Bd CGE1 = G::col_ge(1), CGE2 = G::col_ge(2), CLE2 = G::col_le(C - 2), CLE3 = G::col_le(C - 3);
+
+    {   // horizontal: cell1 = x, cell2 = x+1; token1 = TB[x], token2 = TB[x+1]
+        const Bd spc = z0 | at<1>(z0) | (spec & at<1>(spec));                       // :100-102
+        const Bd condA = G::col_ge(2) & at<-2>(e3) & at<-1>(e2);                     // :42-43
+        const Bd condB = G::col_le(C - 4) & e2 & e3;                                  // :45-46
+        // check_above_and_below(row, c, token2)                                       :48-59
+        const Bd up = RGE1 & at<-C>(ecp1), dn = RLE2 & at<1>(ecm1);
+        const Bd up2 = RGE2 & at<-2 * C>(e2cp1), dn2 = RLE3 & at<1>(e2cm1);
+        const Bd ab1 = (up & dn) | (up.andnot(dn) & up2) | (dn.andnot(up) & dn2);
+        // check_above_and_below(row, c+1, token1)
+        const Bd upb = RGE1 & at<1 - C>(ecm1), dnb = RLE2 & ecp1;
+        const Bd up2b = RGE2 & at<1 - 2 * C>(e2cm1), dn2b = RLE3 & e2cp1;
+        const Bd ab2 = (upb & dnb) | (upb.andnot(dnb) & up2b) | (dnb.andnot(upb) & dn2b);
+        HL = CLE2 & (spc | ((condA | condB | ab1 | ab2).andnot(e1)));                 // :103-104
+    }
+    {   // vertical: cell1 = x (upper), cell2 = x+C; token1 = TB[x], token2 = TB[x+C]
+        const Bd spc = z0 | at<C>(z0) | (spec & at<C>(spec));
+        const Bd condA = G::row_le(R - 4) & e2c & e3c;                               // :75-76
+        const Bd condB = RGE2 & at<-2 * C>(e3c) & at<-C>(e2c);                       // :78-79
+        // check_left_and_right(r+1, c, token1)                                        :81-92
+        const Bd l1 = CGE1 & ecm1, r1 = CLE2 & ecp1, l2 = CGE2 & ecm2, r2 = CLE3 & ecp2;
+        const Bd lr1 = (l1 & r1) | (l1.andnot(r1) & l2) | (r1.andnot(l1) & r2);
+        // check_left_and_right(r, c, token2)
+        const Bd l1b = CGE1 & at<-1>(ecp1), r1b = CLE2 & at<1>(ecm1);
+        const Bd l2b = CGE2 & at<-2>(ecp2), r2b = CLE3 & at<2>(ecm2);
+        const Bd lr2 = (l1b & r1b) | (l1b.andnot(r1b) & l2b) | (r1b.andnot(l1b) & r2b);
+        VL = RLE2 & (spc | ((condA | condB | lr1 | lr2).andnot(ec)));
+    }
+}
+
+// legal bits in action-id order (BoardConfig.actions, boardConfig.py:37,45-59):
+// row r owns ids r*(2C-1) .. ; first C-1 horizontal (r,c)-(r,c+1), then C vertical.
+template <class CF, int ROW = 0>
+M3_HD void action_bits_rows(const typename CF::Bd& HL, const typename CF::Bd& VL, uint32_t* act) {
+    if constexpr (ROW < CF::R) {
+        constexpr int C = CF::C;
+        constexpr int POS = ROW * (2 * C - 1);
+        const uint32_t h = extract_bits<ROW * C, C - 1>(HL);
+        const uint32_t v = extract_bits<ROW * C, C>(VL);
+        const uint32_t f = h | (v << (C - 1));  // 2C-1 <= 31 bits
+        constexpr int q = POS >> 5, s = POS & 31;
+        act[q] |= f << s;
+        if constexpr (s != 0 && s + 2 * C - 1 > 32) act[q + 1] |= f >> (32 - s);
+        action_bits_rows<CF, ROW + 1>(HL, VL, act);
+    }
+}
+template <class CF>
+M3_HD void action_bits(const typename CF::Bd& HL, const typename CF::Bd& VL, uint32_t* act) {
+#pragma unroll
+    for (int i = 0; i < CF::AW; ++i) act[i] = 0u;
+    action_bits_rows<CF, 0>(HL, VL, act);
+}
+
+M3_HD int select_bit(uint32_t u, int k) {  // position of the k-th (0-based) set bit of u
+    int pos = 0;
+#pragma unroll
+    for (int half = 16; half >= 1; half >>= 1) {
+        const uint32_t lo = u & ((1u << half) - 1u);
+        const int c = __builtin_popcount(lo);
+        if (k >= c) {
+            k -= c;
+            u >>= half;
+            pos += half;
+        } else {
+            u = lo;
+        }
+    }
+    return pos;
+}
+
+// np.random.choice(legal_actions) (samplerTasks.py:13): legal[randint(0, len)]
+template <class CF, class RNG>
+M3_HD int random_action(const uint32_t* act, RNG& rng) {
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < CF::AW; ++i) cnt += __builtin_popcount(act[i]);
+    if (cnt == 0) return -1;
+    int k = (int)rand_masked(rng, (uint32_t)(cnt - 1));
+    int res = 0;
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < CF::AW; ++i) {
+        const int c = __builtin_popcount(act[i]);
+        if (!found) {
+            if (k < c) {
+                res = i * 32 + select_bit(act[i], k);
+                found = true;
+            } else {
+                k -= c;
+            }
+        }
+    }
+    return res;
+}
+
+// --------------------------------------------------------------------------
+// get_matches (boardFunctions.py:121-156) + get_match_spawn_mask (:159-169)
+//
+// The reference scans cells row-major, skips cells already in a group, and for
+// a start with a horizontal and/or vertical triple appends the maximal run(s)
+// to the FIRST group sharing a cell (duplicates kept). Facts used here (each
+// follows from the scan order): h-runs are disjoint, v-runs are disjoint, a
+// run's vertical part never meets an earlier run, and its horizontal part can
+// only meet earlier vertical runs. So a group is (Hg = union of its h-runs,
+// Vg = union of its v-runs), cell multiplicity is Hg[x] + Vg[x], and the merge
+// target is the first group with Vg & run_h != 0.
+//
+// Spawn: group with len = |Hg| + |Vg| > 3 gets, at the (len/2)-th cell of its
+// sorted multiset, V/M if it is one h-run (rows equal), H/M if one v-run
+// (cols equal), else B; later groups overwrite. The spawn map is returned as
+// the three value planes BITS..BITS+2 (H = bit BITS, V = bit BITS+1, B = both,
+// M = bit BITS+2).
+// --------------------------------------------------------------------------
+template <class CF>
+struct Groups {
+    typename CF::Bd h[CF::MAXG];
+    typename CF::Bd v[CF::MAXG];
+};
+
+template <class CF>
+M3_HD int multiset_select(const typename CF::Bd& hg, const typename CF::Bd& vg, int k) {
+#pragma unroll
+    for (int i = 0; i < CF::W; ++i) {
+        const int c = __builtin_popcount(hg.w[i]) + __builtin_popcount(vg.w[i]);
+        if (k < c) {
+            uint32_t u = hg.w[i] | vg.w[i];
+            while (u) {
+                const int b = __builtin_ctz(u);
+                const int m = (int)((hg.w[i] >> b) & 1u) + (int)((vg.w[i] >> b) & 1u);
+                if (k < m) return i * 32 + b;
+                k -= m;
+                u &= u - 1u;
+            }
+        }
+        k -= c;
+    }
+    return 0;
+}
+
+template <class CF, bool SPAWN>
+M3_HD bool get_matches(const typename CF::Bd* P, typename CF::Bd& mask, typename CF::Bd* sw) {
+    using Bd = typename CF::Bd;
+    using G = typename CF::G;
+    constexpr int C = CF::C, R = CF::R;
+    constexpr Bd CLE2 = G::col_le(C - 2), RLE2 = G::row_le(R - 2);
+
+    const Bd nz = tb_nonzero<CF>(P);
+    const Bd e1h = CLE2 & tb_eq<CF, 1>(P);   // TB[x] == TB[x+1], same row
+    const Bd e1v = RLE2 & tb_eq<CF, C>(P);   // TB[x] == TB[x+C]
+    const Bd h3 = nz & e1h & at<1>(e1h);     // :138 horizontal triple starts here
+    const Bd v3 = nz & e1v & at<C>(e1v);     // :147 vertical triple starts here
+    Bd cand = h3 | v3;
+    mask = Bd::zero();
+    if constexpr (SPAWN) {
+        sw[0] = Bd::zero();
+        sw[1] = Bd::zero();
+        sw[2] = Bd::zero();
+    }
+    if (!cand.any()) return false;
+
+    // doubling link masks for run floods (runs are <= 16 long)
+    const Bd dh2 = e1h & at<1>(e1h), dh4 = dh2 & at<2>(dh2), dh8 = dh4 & at<4>(dh4);
+    const Bd dv2 = e1v & at<C>(e1v), dv4 = dv2 & at<2 * C>(dv2), dv8 = dv4 & at<4 * C>(dv4);
+
+    Groups<CF> grp;
+    int ng = 0;
+    Bd vruns = Bd::zero();
+    while (cand.any()) {                                       // row-major scan over run starts
+        const int x = cand.lowest();
+        const Bd bx = Bd::bit_at(x);
+        Bd rh = Bd::zero(), rv = Bd::zero();
+        if ((h3 & bx).any()) {                                 // :138-144 extend right
+            rh = bx;
+            rh |= at<-1>(rh & e1h);
+            rh |= at<-2>(rh & dh2);
+            rh |= at<-4>(rh & dh4);
+            if constexpr (C > 8) rh |= at<-8>(rh & dh8);
+        }
+        if ((v3 & bx).any()) {                                 // :147-153 extend down
+            rv = bx;
+            rv |= at<-C>(rv & e1v);
+            rv |= at<-2 * C>(rv & dv2);
+            rv |= at<-4 * C>(rv & dv4);
+            if constexpr (R > 8) rv |= at<-8 * C>(rv & dv8);
+        }
+        const Bd run = rh | rv;
+        mask |= run;
+        cand = cand.andnot(run | bx);                           // later starts inside a run are skipped (:136)
+        if constexpr (SPAWN) {
+            int g = -1;
+            if ((rh & vruns).any()) {                          // add_to_matches (:126-131)
+                for (int gi = 0; gi < ng; ++gi) {
+                    if ((grp.v[gi] & rh).any()) { g = gi; break; }
+                }
+            }
+            if (g < 0) {
+                g = ng++;
+                grp.h[g] = rh;
+                grp.v[g] = rv;
+            } else {
+                grp.h[g] |= rh;
+                grp.v[g] |= rv;
+            }
+            vruns |= rv;
+        }
+    }
+    if constexpr (SPAWN) {
+        for (int gi = 0; gi < ng; ++gi) {                      // get_match_spawn_mask (:159-169)
+            const Bd hg = grp.h[gi], vg = grp.v[gi];
+            const int len = hg.popc() + vg.popc();
+            if (len <= 3) continue;
+            int centre, kind;  // kind bits: 1 = plane BITS, 2 = BITS+1, 4 = BITS+2
+            if (!vg.any()) {                                   // all rows equal
+                centre = hg.lowest() + len / 2;
+                kind = len > 4 ? 4 : 2;                        // M : V
+            } else if (!hg.any()) {                            // all cols equal
+                centre = vg.lowest() + (len / 2) * C;
+                kind = len > 4 ? 4 : 1;                        // M : H
+            } else {
+                centre = multiset_select<CF>(hg, vg, len / 2);
+                kind = 3;                                      // B
+            }
+            const Bd bm = Bd::bit_at(centre);
+            sw[0] = sw[0].andnot(bm);
+            sw[1] = sw[1].andnot(bm);
+            sw[2] = sw[2].andnot(bm);
+            if (kind & 1) sw[0] |= bm;
+            if (kind & 2) sw[1] |= bm;
+            if (kind & 4) sw[2] |= bm;
+        }
+    }
+    return true;
+}
+
+// --------------------------------------------------------------------------
+// cascade pieces (boardv2.py:138-202)
+// --------------------------------------------------------------------------
+// Python slice a[start:stop] on an axis of length n (start may be -1)
+M3_HD void py_slice(int start, int stop, int n, int& lo, int& hi) {
+    if (start < 0) {
+        start += n;
+        if (start < 0) start = 0;
+    }
+    if (start > n) start = n;
+    if (stop > n) stop = n;
+    lo = start;
+    hi = stop > start ? stop : start;
+}
+
+// special tokens whose TB is zero fire (:141-154); SP is not refreshed inside
+// the pass, so the effects are a union and order does not matter.
+template <class CF, int NPU>
+M3_HD typename CF::Bd fire_specials(const typename CF::Bd* P, typename CF::Bd z) {
+    using Bd = typename CF::Bd;
+    using G = typename CF::G;
+    constexpr int BITS = CF::BITS, C = CF::C, R = CF::R;
+    const Bd spz = z & special_mask<CF, NPU>(P);
+    const Bd kh = P[BITS].andnot(P[BITS + 1]);   // (x & STM) == H
+    const Bd kv = P[BITS + 1].andnot(P[BITS]);   // (x & STM) == V
+    const Bd kb = P[BITS] & P[BITS + 1];         // (x & STM) == B
+    Bd trig = spz & (kh | kv | kb);
+    Bd add = Bd::zero();
+    while (trig.any()) {
+        const int x = trig.lowest();
+        trig.pop_lowest();
+        const int i = x / C, j = x % C;
+        if (kh.test(x)) {
+            add |= G::row_band(i, i + 1);                   // token_board[i, :] = 0
+        } else if (kv.test(x)) {
+            add |= G::col_band(j, j + 1);                   // token_board[:, j] = 0
+        } else {                                            // token_board[j-1:j+1, i-1:i+1] = 0
+            int rl, rh, cl, ch;
+            py_slice(j - 1, j + 1, R, rl, rh);
+            py_slice(i - 1, i + 1, C, cl, ch);
+            add |= G::row_band(rl, rh) & G::col_band(cl, ch);
+        }
+    }
+    return z | add;
+}
+
+// reward += sum(points[TB == 0]) with point_board_vec (:58-65, :157-158)
+template <class CF, int NPU>
+M3_HD int score(const typename CF::Bd* P, const typename CF::Bd& z) {
+    using Bd = typename CF::Bd;
+    constexpr int BITS = CF::BITS;
+    const Bd spec = special_mask<CF, NPU>(P);
+    Bd hi2 = P[BITS + 2];
+#pragma unroll
+    for (int p = BITS + 3; p < NPU; ++p) hi2 |= P[p];
+    Bd other = P[0];
+#pragma unroll
+    for (int p = 1; p < NPU; ++p)
+        if (p != BITS + 2) other |= P[p];
+    const Bd eqm = P[BITS + 2].andnot(other);                  // x == M
+    const Bd kb = P[BITS] & P[BITS + 1];
+    const Bd lt = spec.andnot(hi2 | kb);                       // TM < x < STM
+    const Bd zs = z & spec;
+    const int n_all = z.popc(), n_spec = zs.popc();
+    const int n_m = (z & eqm).popc(), n_lt = (z & lt).popc();
+    return 2 * (n_all - n_spec) + 250 * n_m + 25 * n_lt + 50 * (n_spec - n_m - n_lt);
+}
+
+// next_state[TB==0] = 0; next_state += spawn; clip(0, 32)   (:161-163)
+template <class CF, int NPU>
+M3_HD void merge_clip(typename CF::Bd* P, const typename CF::Bd& z, const typename CF::Bd* sw) {
+    using Bd = typename CF::Bd;
+    constexpr int BITS = CF::BITS;
+#pragma unroll
+    for (int p = 0; p < NPU; ++p) P[p] = P[p].andnot(z);
+    P[BITS] |= sw[0];
+    P[BITS + 1] |= sw[1];
+    P[BITS + 2] |= sw[2];
+    // > 32: bit 5 with any lower bit, or bit 6
+    Bd low = P[0];
+#pragma unroll
+    for (int p = 1; p < 5; ++p) low |= P[p];
+    // plane 6 holds input values >= 64 (first pass) or a spawned M = 64 on
+    // 4-bit-type boards; both clip to 32
+    const Bd cl = (P[5] & low) | P[6];
+#pragma unroll
+    for (int p = 0; p < 5; ++p) P[p] = P[p].andnot(cl);
+    P[5] |= cl;
+    P[6] = Bd::zero();
+}
+
+// gravity + refill (:166-173). Columns left to right, new tiles on top in draw
+// order (new[0] at row 0). Tiles come from randint(1, T+1).
+template <class CF, class RNG>
+M3_HD void gravity_refill(typename CF::Bd* P, RNG& rng) {
+    using Bd = typename CF::Bd;
+    using G = typename CF::G;
+    constexpr int C = CF::C, R = CF::R, NPU = 6;
+    constexpr Bd VALID = G::valid();
+    Bd occ = P[0];
+#pragma unroll
+    for (int p = 1; p < NPU; ++p) occ |= P[p];
+    for (;;) {  // drop every tile that has a hole somewhere below it by one row
+        const Bd e = VALID.andnot(occ);
+        Bd s = at<C>(e);
+        s |= at<C>(s);
+        s |= at<2 * C>(s);
+        s |= at<4 * C>(s);
+        if constexpr (R > 9) s |= at<8 * C>(s);
+        const Bd mv = occ & s;
+        if (!mv.any()) break;
+#pragma unroll
+        for (int p = 0; p < NPU; ++p) {
+            const Bd m = P[p] & mv;
+            P[p] = P[p].andnot(mv) | at<-C>(m);
+        }
+        occ = occ.andnot(mv) | at<-C>(mv);
+    }
+    Bd em = VALID.andnot(occ);              // top-aligned empty cells
+    if (!em.any()) return;
+    uint32_t tops = em.w[0] & ((1u << C) - 1u);  // columns with at least one empty cell
+    int c = __builtin_ctz(tops);
+    int r = 0;
+    constexpr uint32_t RNGT = (uint32_t)(CF::T - 1);
+    for (;;) {
+        const uint32_t v = rand_masked(rng, RNGT) + 1u;   // randint(1, T+1)
+        const int x = r * C + c;
+        const Bd bm = Bd::bit_at(x);
+#pragma unroll
+        for (int p = 0; p < CF::BITS; ++p) {
+            const uint32_t on = 0u - ((v >> p) & 1u);
+#pragma unroll
+            for (int i = 0; i < CF::W; ++i) P[p].w[i] |= bm.w[i] & on;
+        }
+        if (r + 1 < R && em.test(x + C)) {
+            ++r;
+        } else {
+            tops &= ~(1u << c);
+            if (!tops) break;
+            c = __builtin_ctz(tops);
+            r = 0;
+        }
+        if (rng.overflow) break;
+    }
+}
+
+// shuffle (boardFunctions.py:16-23): reseed, Fisher-Yates over rows with
+// random_interval, then put every special back at its original cell.
+template <class CF, class RNG>
+M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng) {
+    using Bd = typename CF::Bd;
+    constexpr int C = CF::C, R = CF::R, NPU = 6;
+    rng.reseed();
+    const Bd sp = special_mask<CF, NPU>(P);
+    uint64_t idx = 0;  // nibble i = source row of row i
+#pragma unroll
+    for (int i = 0; i < R; ++i) idx |= (uint64_t)i << (4 * i);
+    for (int i = R - 1; i >= 1; --i) {
+        const int j = (int)rand_masked(rng, (uint32_t)i);
+        const uint64_t a = (idx >> (4 * i)) & 0xFull, b = (idx >> (4 * j)) & 0xFull;
+        idx &= ~((0xFull << (4 * i)) | (0xFull << (4 * j)));
+        idx |= (b << (4 * i)) | (a << (4 * j));
+    }
+    Bd out[NPU];
+#pragma unroll
+    for (int p = 0; p < NPU; ++p) out[p] = Bd::zero();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int src = (int)((idx >> (4 * i)) & 0xFull);
+        const int sb = src * C;
+        const int q = sb >> 5, s = sb & 31;
+#pragma unroll
+        for (int p = 0; p < NPU; ++p) {
+            const uint32_t lo = P[p].word_at(q), hi = P[p].word_at(q + 1);
+            uint32_t f = s ? ((lo >> s) | (hi << ((32 - s) & 31))) : lo;
+            f &= (1u << C) - 1u;
+            const int dpos = i * C;
+            const int dq = dpos >> 5, ds = dpos & 31;
+            out[p].w[dq] |= f << ds;
+            if (ds + C > 32 && dq + 1 < CF::W) out[p].w[dq + 1] |= f >> (32 - ds);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NPU; ++p) P[p] = out[p].andnot(sp) | (P[p] & sp);
+}
+
+// --------------------------------------------------------------------------
+// BoardV2.apply_action (boardv2.py:43-207)
+// P: NP planes in/out. Returns the step reward; sets flags/draws and the
+// legal masks of the resulting board.
+// --------------------------------------------------------------------------
+template <class CF, class RNG>
+M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, uint32_t& flags,
+                       typename CF::Bd& HL, typename CF::Bd& VL) {
+    using Bd = typename CF::Bd;
+    using G = typename CF::G;
+    constexpr int C = CF::C, R = CF::R, BITS = CF::BITS, TM = CF::TM;
+    constexpr int H = CF::H, V = CF::V, B = CF::B, M = CF::M;
+    constexpr Bd VALID = G::valid();
+    flags = 0u;
+    if (n_actions < 1 || action < 0 || action >= CF::A) {      // :44-45, KeyError at :48
+        flags = (n_actions < 1) ? FLAG_TERMINAL : FLAG_BAD_ACTION;
+        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
+        return 0;
+    }
+    rng.reseed();                                               // :46
+    // decode (boardConfig.py:45-59)
+    constexpr int AR = 2 * C - 1, BR = C - 1;
+    int sr, sc, tr, tc;
+    if (action % AR >= BR) {
+        sc = action % AR - BR;
+        sr = (action - 3 - sc) / AR;
+        tr = sr + 1;
+        tc = sc;
+    } else {
+        sc = action % AR;
+        sr = (action - sc) / AR;
+        tr = sr;
+        tc = sc + 1;
+    }
+    const int s = sr * C + sc, t = tr * C + tc;
+    const int tok1 = cell_value<CF, CF::NP>(P, s), tok2 = cell_value<CF, CF::NP>(P, t);  // :73
+    {   // swap (:51, boardFunctions.py:115-118)
+        const Bd st = Bd::bit_at(s) | Bd::bit_at(t);
+        const int d = tok1 ^ tok2;
+#pragma unroll
+        for (int p = 0; p < CF::NP; ++p)
+            if ((d >> p) & 1) P[p] ^= st;
+    }
+    const int ty1 = tok2 > TM ? tok2 : 0, ty2 = tok1 > TM ? tok1 : 0;  // special_tokens[source/target] :74
+    auto are = [&](int a, int b) { return (ty1 == a && ty2 == b) || (ty2 == a && ty1 == b); };  // :76-77
+
+    Bd sw[3] = {Bd::zero(), Bd::zero(), Bd::zero()};
+    Bd zr;
+    if (are(M, M)) {                                            // :81-82
+        zr = VALID;
+    } else if (are(M, B) || are(M, H) || are(M, V) || are(M, 0)) {
+        zr = Bd::zero();  // :84-103 select TB == max(token1, token2) == M: empty by construction
+    } else if (are(B, B)) {                                     // :112-116
+        const int r0 = tr - 2 < 0 ? 0 : tr - 2, r1 = tr + 2 > R ? R : tr + 2;
+        const int c0 = tc - 2 < 0 ? 0 : tc - 2, c1 = tc + 2 > C ? C : tc + 2;
+        zr = G::row_band(r0, r1) & G::col_band(c0, c1);
+    } else if (are(B, H) || are(B, V)) {                        // :123-125
+        const int r0 = tr - 2 < 0 ? 0 : tr - 2, r1 = tr + 2 > R ? R : tr + 2;
+        const int c0 = tc - 2 < 0 ? 0 : tc - 2, c1 = tc + 2 > C ? C : tc + 2;
+        zr = G::col_band(c0, c1) | G::row_band(r0, r1);
+    } else if (are(H, V)) {                                     // :130-132 rows < t.col, rows >= t.row
+        zr = G::row_band(0, tc < R ? tc : R) | G::row_band(tr, R);
+    } else {                                                    // :133-136
+        get_matches<CF, true>(P, zr, sw);
+    }
+    int reward = 0;
+    // first pass with all 7 planes (input values may exceed 32 until the clip)
+    Bd z = zr | VALID.andnot(tb_nonzero<CF>(P));
+    z = fire_specials<CF, CF::NP>(P, z);
+    reward += score<CF, CF::NP>(P, z);
+    merge_clip<CF, CF::NP>(P, z, sw);
+    for (;;) {                                                  // :138
+        gravity_refill<CF>(P, rng);                             // :166-173
+        if (rng.overflow) break;
+        Bd mask;
+        bool found = get_matches<CF, true>(P, mask, sw);        // :176-181
+        if (!found) {
+            legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
+            int shuffles = 0;
+            while (!found && !(HL.any() || VL.any())) {          // :188-194
+                if (shuffles >= CF::SHUFFLE_CAP) {
+                    flags |= FLAG_SHUFFLE_CAP;
+                    break;
+                }
+                shuffle_rows<CF>(P, rng);
+                flags |= FLAG_SHUFFLED;
+                ++shuffles;
+                found = get_matches<CF, true>(P, mask, sw);
+                if (!found) legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
+            }
+            if (!found) break;                                   // :195-196
+        }
+        z = mask | VALID.andnot(tb_nonzero<CF>(P));            // :199 + TB==0 cells
+        z = fire_specials<CF, 6>(P, z);
+        reward += score<CF, 6>(P, z);
+        merge_clip<CF, 6>(P, z, sw);
+    }
+    if (rng.overflow) flags |= FLAG_RNG_OVERFLOW;
+    return reward;
+}
+
+// --------------------------------------------------------------------------
+// BoardV2.__init__ with array=None (boardv2.py:17-27). mt must be freshly
+// seeded. Writes the planes (values 1..T).
+// --------------------------------------------------------------------------
+template <class CF, class RNG>
+M3_HD void init_board(typename CF::Bd* P, RNG& mt) {
+    using Bd = typename CF::Bd;
+    constexpr uint32_t RNGT = (uint32_t)(CF::T - 1);
+#pragma unroll
+    for (int p = 0; p < CF::NP; ++p) P[p] = Bd::zero();
+    for (int x = 0; x < CF::N; ++x) {                          // :21 randint(1, T+1, (R, C))
+        const uint32_t v = rand_masked(mt, RNGT) + 1u;
+        const Bd bm = Bd::bit_at(x);
+#pragma unroll
+        for (int p = 0; p < CF::BITS; ++p) {
+            const uint32_t on = 0u - ((v >> p) & 1u);
+#pragma unroll
+            for (int i = 0; i < CF::W; ++i) P[p].w[i] |= bm.w[i] & on;
+        }
+    }
+    Bd mask;
+    Bd* none = nullptr;
+    while (get_matches<CF, false>(P, mask, none)) {            // :23-27
+        for (int x = 0; x < CF::N; ++x) {
+            const uint32_t v = rand_masked(mt, RNGT) + 1u;
+            if (mask.test(x)) set_cell<CF, CF::BITS>(P, x, (int)v);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// planes <-> int8 cells. Eight cells at a time: an 8x8 bit-matrix transpose
+// turns 8 bytes (cell-major) into 8 plane bytes (plane-major) and back.
+// --------------------------------------------------------------------------
+M3_HD void transpose8(uint32_t& lo, uint32_t& hi) {
+    uint32_t t;
+    t = (lo ^ (lo >> 7)) & 0x00AA00AAu; lo ^= t ^ (t << 7);
+    t = (hi ^ (hi >> 7)) & 0x00AA00AAu; hi ^= t ^ (t << 7);
+    t = (lo ^ (lo >> 14)) & 0x0000CCCCu; lo ^= t ^ (t << 14);
+    t = (hi ^ (hi >> 14)) & 0x0000CCCCu; hi ^= t ^ (t << 14);
+    t = (lo ^ (hi << 4)) & 0xF0F0F0F0u; lo ^= t; hi ^= t >> 4;
+}
+
+// cells: N bytes as little-endian 32-bit words, cw[q] holds cells 4q..4q+3
+template <class CF>
+M3_HD void planes_from_words(const uint32_t* cw, typename CF::Bd* P) {
+    constexpr int NW = (CF::N + 3) / 4;
+#pragma unroll
+    for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+#pragma unroll
+    for (int g = 0; g < (CF::N + 7) / 8; ++g) {
+        uint32_t lo = (2 * g < NW) ? cw[2 * g] : 0u;
+        uint32_t hi = (2 * g + 1 < NW) ? cw[2 * g + 1] : 0u;
+        transpose8(lo, hi);
+        const int q = (8 * g) >> 5, sh = (8 * g) & 31;
+#pragma unroll
+        for (int p = 0; p < CF::NP; ++p) {
+            const uint32_t byte = ((p < 4 ? lo : hi) >> (8 * (p & 3))) & 0xFFu;
+            P[p].w[q] |= byte << sh;
+        }
+    }
+    constexpr typename CF::Bd VALID = CF::G::valid();
+#pragma unroll
+    for (int p = 0; p < CF::NP; ++p) P[p] &= VALID;
+}
+
+template <class CF>
+M3_HD void words_from_planes(const typename CF::Bd* P, uint32_t* cw) {
+    constexpr int NW = (CF::N + 3) / 4;
+#pragma unroll
+    for (int g = 0; g < (CF::N + 7) / 8; ++g) {
+        const int q = (8 * g) >> 5, sh = (8 * g) & 31;
+        uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+        for (int p = 0; p < CF::NP; ++p) {
+            const uint32_t byte = (P[p].w[q] >> sh) & 0xFFu;
+            if (p < 4) lo |= byte << (8 * p);
+            else hi |= byte << (8 * (p - 4));
+        }
+        transpose8(lo, hi);
+        if (2 * g < NW) cw[2 * g] = lo;
+        if (2 * g + 1 < NW) cw[2 * g + 1] = hi;
+    }
+}
+
+}  // namespace m3

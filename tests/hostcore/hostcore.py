@@ -1,0 +1,90 @@
+"""ctypes face of the TEST-ONLY host build of the device rule code (hostcore.hip)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libhostcore.so")
+SRC = [os.path.join(HERE, "hostcore.hip")] + [
+    os.path.join(HERE, "..", "..", "element-crush-gym_amd", "csrc", f) for f in
+    ("m3_rules.hpp", "m3_bitboard.hpp", "m3_rng.hpp")]
+_lib = None
+CFG_ID = {(9, 9, 6): 0, (16, 16, 8): 1}
+AW = {(9, 9, 6): 5, (16, 16, 8): 15}
+
+
+def build():
+    newest = max(os.path.getmtime(s) for s in SRC)
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
+        return
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", "-shared",
+                    "-o", LIB, SRC[0]], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(LIB)
+        _lib.hc_chain_draw.restype = ctypes.c_uint32
+        _lib.hc_chain_draw.argtypes = [ctypes.c_uint32, ctypes.c_int]
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class HostCore:
+    def __init__(self, R=9, C=9, T=6):
+        self.shape = (R, C, T)
+        self.cfg = CFG_ID[(R, C, T)]
+        self.N = R * C
+        self.aw = AW[(R, C, T)]
+
+    def apply(self, boards, seeds, n_actions, actions):
+        boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
+        n = len(boards)
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        na = np.ascontiguousarray(np.broadcast_to(n_actions, (n,)), dtype=np.int32)
+        acts = np.ascontiguousarray(actions, dtype=np.int32)
+        out = np.zeros_like(boards)
+        rew = np.zeros(n, np.int32); drw = np.zeros(n, np.int32); flg = np.zeros(n, np.int32)
+        legal = np.zeros((n, self.aw), np.uint32); nxt = np.zeros(n, np.int32)
+        lib().hc_apply(self.cfg, ctypes.c_long(n), _p(boards), _p(seeds), _p(na), _p(acts), _p(out), _p(rew),
+                       _p(drw), _p(flg), _p(legal), _p(nxt))
+        return out, rew, drw, flg, legal, nxt
+
+    def init(self, seeds):
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        n = len(seeds)
+        out = np.zeros((n, self.N), np.int8); drw = np.zeros(n, np.int32)
+        m397 = np.zeros(n, np.uint32); fa = np.zeros(n, np.int32)
+        lib().hc_init(self.cfg, ctypes.c_long(n), _p(seeds), _p(out), _p(drw), _p(m397), _p(fa))
+        return out, drw, m397, fa
+
+    def legal(self, boards):
+        boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
+        out = np.zeros((len(boards), self.aw), np.uint32)
+        lib().hc_legal(self.cfg, ctypes.c_long(len(boards)), _p(boards), _p(out))
+        return out
+
+    def matches(self, tbs):
+        tbs = np.ascontiguousarray(tbs, dtype=np.int8).reshape(-1, self.N)
+        n = len(tbs)
+        mask = np.zeros((n, self.N), np.uint8); sp = np.zeros((n, self.N), np.int32); fd = np.zeros(n, np.int32)
+        lib().hc_matches(self.cfg, ctypes.c_long(n), _p(tbs), _p(mask), _p(sp), _p(fd))
+        return mask, sp, fd
+
+    def roundtrip(self, boards):
+        boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
+        out = np.zeros_like(boards)
+        lib().hc_roundtrip(self.cfg, ctypes.c_long(len(boards)), _p(boards), _p(out))
+        return out
+
+
+def bits_to_list(words, A):
+    bits = np.unpackbits(np.asarray(words, dtype="<u4").view(np.uint8), bitorder="little")[:A]
+    return [int(i) for i in np.nonzero(bits)[0]]
