@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched Match3Env.step throughput on MI355X (BASELINE.json metric).
+
+One "step" = one env step of every board on every GPU: the fused HIP step
+kernel (swap, combos, cascade fixed point, MT19937 refill, dead-board
+shuffle, scoring, legal mask, next seeded random action), the overflow-fixup
+launch, and the autoreset launch that re-initialises finished boards
+(seed += stride); for N > 1 also the RCCL all-gather of packed
+reward/truncated/done over xGMI. Inputs are resident in HBM before timing.
+
+    python bench.py [--gpus N --steps K --warmup W --boards B]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "element-crush-gym_amd")
+for p in (PKG, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "env-steps/sec (batched boards) at 1/2/4/8 MI355X, 9×9×6; bit-exact vs CPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def algorithmic_bytes_per_step(rows, cols):
+    """board in+out (2*R*C int8) + action 2 + reward 4 + done 1 + moves 2 + score 8 + seed 4."""
+    return 2 * rows * cols + 21
+
+
+def cpu_baseline(rows, cols, types, moves, goal, seconds):
+    """The C oracle (bit-exact port of the reference step) on this host's cores, bounded sample."""
+    from oracle import Oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    o = Oracle(rows, cols, types)
+    probe = 2048
+    t0 = time.perf_counter()
+    steps, _ = o.run_episodes(list(range(10**6, 10**6 + probe)), moves, goal, threads)
+    dt = time.perf_counter() - t0
+    n = max(probe, int(probe * seconds / max(dt, 1e-3)))
+    seeds = list(range(2 * 10**6, 2 * 10**6 + n))
+    t0 = time.perf_counter()
+    steps, _ = o.run_episodes(seeds, moves, goal, threads)
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} seeded {rows}x{cols}x{types} random-action episodes of {moves} moves "
+                      f"(init + legal_actions + choice + apply_action per move; {steps} steps, {dt:.1f} s), "
+                      "oracle/m3_oracle.c, OpenMP over episodes"}
+
+
+def load_traffic(shape_tag, boards):
+    """HBM bytes/launch of the step kernel from the committed rocprofv3 PMC summary, if one matches."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("shape") == shape_tag and int(t.get("boards")) == boards:
+            return float(t["hbm_bytes_per_launch"])
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--boards", type=int, default=1 << 20, help="boards per GPU (C3: 1,048,576)")
+    ap.add_argument("--shape", default="9x9x6")
+    ap.add_argument("--moves", type=int, default=20)
+    ap.add_argument("--goal", type=int, default=500)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rows, cols, types = (int(x) for x in args.shape.split("x"))
+
+    if not os.path.exists(os.path.join(PKG, "build", "libm3.so")):
+        subprocess.run(["make", "-C", PKG], check=True)
+    from match3tile.batched import BatchedMatch3Env
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # host-side rendezvous / barrier / max only (gloo)
+
+        dist.init_process_group("gloo")
+
+    B = args.boards
+    env = BatchedMatch3Env(B, rows, cols, types, num_moves=args.moves, env_goal=args.goal, device=local,
+                           seed_base=1 + rank * B, autoreset=True, seed_stride=world * B)
+    if world > 1:
+        obj = [env.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        env.init_comm(obj[0], world, rank)
+
+    def step():
+        env.step()
+        if world > 1:
+            env.gather()
+
+    for _ in range(args.warmup):
+        step()
+    env.synchronize()
+    if dist:
+        dist.barrier()
+    env.enable_timing(args.steps)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    env.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kms = env.kernel_ms()
+    env.close()
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    total_steps = world * B * args.steps
+    value = total_steps / elapsed
+    avg_kernel_s = float(kms.mean()) / 1e3 if len(kms) else float("nan")
+    bytes_per_launch = B * algorithmic_bytes_per_step(rows, cols)
+    achieved = bytes_per_launch / avg_kernel_s / 1e9
+    traffic = load_traffic(args.shape, B)
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic: seeded initial boards (seed = 1 + board index), seeded random_action per move "
+                "(samplerTasks.random_task contract), 20-move episodes, autoreset with seed += n_boards",
+        "config": {
+            "workload": f"C3: {B:,} boards per GPU, {rows}x{cols}x{types}, Match3Env.step x {args.steps} "
+                        "(step kernel + overflow fixup + autoreset; RCCL reward/done all-gather when N>1)",
+            "boards_per_gpu": B,
+            "shape": args.shape,
+            "num_moves": args.moves,
+            "env_goal": args.goal,
+            "parallelism": f"dp{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_env_step",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "avg_kernel_ms": avg_kernel_s * 1e3,
+            "note": "integer-VALU bound path; HBM roofline per BASELINE/SURVEY §8(d): 183 B per 9x9 env-step",
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(rows, cols, types, args.moves, args.goal, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

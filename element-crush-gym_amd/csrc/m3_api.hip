@@ -1,0 +1,994 @@
+// m3_api.hip -- gfx950 kernels + the C ABI of include/m3.h.
+//
+// Kernel shape (all step kernels): one board per lane, 256-lane workgroups
+// (4 wave64s). Boards are int8 [n][R*C] in HBM. A workgroup stages its 256
+// boards (256*81 = 20,736 B at 9x9) HBM -> LDS with 16-byte coalesced loads;
+// each lane reads its own board out of LDS as dwords and transposes it into 7
+// bit-planes in VGPRs, runs the whole fixed-point step in registers
+// (m3_rules.hpp), writes the result back into its LDS slot, and the
+// workgroup streams the 256 boards out with 16-byte stores. Per-board scalars
+// (seed, mt[397], score, moves, pre-drawn action) are SoA and coalesced.
+//
+// The step uses ChainMT (register-only MT19937). A step that needs >= 624
+// draws (never observed in play; possible in principle) appends its index to
+// an overflow list and is redone by k_*_fix with the 624-word FullMT in
+// scratch. That kernel reads the untouched input buffer (boards ping-pong),
+// so the result is still exact.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/m3.h"
+#include "m3_rules.hpp"
+
+using namespace m3;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int set_err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return set_err(M3_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                           __LINE__);                                                            \
+    } while (0)
+
+#define RCCL_TRY(expr)                                                                            \
+    do {                                                                                          \
+        ncclResult_t r_ = (expr);                                                                 \
+        if (r_ != ncclSuccess) return set_err(M3_ERR_RCCL, "%s: %s", #expr, ncclGetErrorString(r_)); \
+    } while (0)
+
+#define CHECK_ARG(cond, msg)                                       \
+    do {                                                           \
+        if (!(cond)) return set_err(M3_ERR_INVALID, "%s", (msg)); \
+    } while (0)
+
+constexpr int BLOCK = 256;
+constexpr int FIX_BLOCK = 64;
+constexpr int FIX_GRID = 256;
+
+// ---------------------------------------------------------------------------
+// LDS staging
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void block_copy_in(const int8_t* __restrict__ g, uint8_t* lds, int nb) {
+    const int bytes = nb * N;
+    const int n16 = bytes >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(g);
+    uint4* d4 = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < n16; i += BLOCK) d4[i] = s4[i];
+    for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) lds[i] = (uint8_t)g[i];
+}
+
+template <int N>
+__device__ __forceinline__ void block_copy_out(int8_t* __restrict__ g, const uint8_t* lds, int nb) {
+    const int bytes = nb * N;
+    const int n16 = bytes >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(lds);
+    uint4* d4 = reinterpret_cast<uint4*>(g);
+    for (int i = threadIdx.x; i < n16; i += BLOCK) d4[i] = s4[i];
+    for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) g[i] = (int8_t)lds[i];
+}
+
+// lane's board (N bytes at lds + slot*N, any alignment) -> bit-planes.
+// The dword window may reach into the neighbour's bytes; planes_from_words
+// masks every bit >= N.
+template <class CF>
+__device__ __forceinline__ void lds_to_planes(const uint8_t* lds, int slot, typename CF::Bd* P) {
+    constexpr int NW = (CF::N + 3) / 4;
+    const int off = slot * CF::N;
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(lds + (off & ~3));
+    const uint32_t sh = (uint32_t)(off & 3) * 8u;
+    uint32_t cw[NW];
+    uint32_t prev = d[0];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+        const uint32_t next = d[q + 1];
+        cw[q] = __builtin_amdgcn_alignbit(next, prev, sh);
+        prev = next;
+    }
+    planes_from_words<CF>(cw, P);
+}
+
+template <class CF>
+__device__ __forceinline__ void planes_to_bytes(const typename CF::Bd* P, uint8_t* dst) {
+    constexpr int NW = (CF::N + 3) / 4;
+    uint32_t cw[NW];
+    words_from_planes<CF>(P, cw);
+#pragma unroll
+    for (int x = 0; x < CF::N; ++x) dst[x] = (uint8_t)(cw[x >> 2] >> (8 * (x & 3)));
+}
+
+template <class CF>
+__device__ __forceinline__ void bytes_to_planes(const int8_t* src, typename CF::Bd* P) {
+    constexpr int NW = (CF::N + 3) / 4;
+    uint32_t cw[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int x = 4 * q + k;
+            if (x < CF::N) v |= (uint32_t)(uint8_t)src[x] << (8 * k);
+        }
+        cw[q] = v;
+    }
+    planes_from_words<CF>(cw, P);
+}
+
+template <class CF>
+__device__ __forceinline__ void store_legal(uint32_t* out, const uint32_t* act) {
+#pragma unroll
+    for (int i = 0; i < CF::AW; ++i) out[i] = act[i];
+}
+
+// ---------------------------------------------------------------------------
+// stateless kernels (BoardV2 facade): m3_apply_actions / m3_init_boards /
+// m3_legal_actions
+// ---------------------------------------------------------------------------
+struct ApplyArgs {
+    int64_t n;
+    const int8_t* boards;
+    const uint32_t* seeds;
+    const int32_t* n_actions;
+    const int32_t* actions;
+    int8_t* out_boards;
+    int32_t* reward;
+    uint32_t* draws;
+    uint32_t* flags;
+    uint32_t* legal;       // nullable
+    int32_t* next_action;  // nullable
+    uint32_t* ovf_count;
+    uint32_t* ovf_list;
+};
+
+// one full apply_action + outputs for board b; returns false on RNG overflow
+template <class CF, class RNG>
+__device__ __forceinline__ bool apply_and_emit(typename CF::Bd* P, const ApplyArgs& a, int64_t b, RNG& rng) {
+    typename CF::Bd HL, VL;
+    uint32_t f;
+    const int r = apply_action<CF>(P, a.n_actions[b], a.actions[b], rng, f, HL, VL);
+    if (f & FLAG_RNG_OVERFLOW) return false;
+    const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
+    a.reward[b] = r;
+    a.draws[b] = stepped ? rng.k : 0u;
+    uint32_t act[CF::AW];
+    action_bits<CF>(HL, VL, act);
+    int na = -1;
+    if (stepped) {
+        na = random_action<CF>(act, rng);
+        if (na < 0) f |= FLAG_NO_LEGAL;
+    }
+    a.flags[b] = f;
+    if (a.next_action) a.next_action[b] = na;
+    if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
+    return true;
+}
+
+template <class CF>
+__global__ void __launch_bounds__(BLOCK) k_apply(ApplyArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BLOCK * CF::N + 16];
+    const int64_t b0 = (int64_t)blockIdx.x * BLOCK;
+    const int nb = (int)((a.n - b0) < BLOCK ? (a.n - b0) : BLOCK);
+    block_copy_in<CF::N>(a.boards + b0 * CF::N, lds, nb);
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < nb) {
+        const int64_t b = b0 + t;
+        typename CF::Bd P[CF::NP];
+        lds_to_planes<CF>(lds, t, P);
+        const uint32_t s = a.seeds[b];
+        ChainMT rng;
+        rng.init(s, mt_state397(s));
+        if (!apply_and_emit<CF>(P, a, b, rng)) {
+            const uint32_t slot = atomicAdd(a.ovf_count, 1u);
+            a.ovf_list[slot] = (uint32_t)b;
+        }
+        planes_to_bytes<CF>(P, lds + t * CF::N);
+    }
+    __syncthreads();
+    block_copy_out<CF::N>(a.out_boards + b0 * CF::N, lds, nb);
+}
+
+// redo overflowed boards with the full 624-word state (lane-private scratch)
+template <class CF>
+__global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
+    const uint32_t cnt = *a.ovf_count;
+    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
+        const int64_t b = a.ovf_list[i];
+        typename CF::Bd P[CF::NP];
+        bytes_to_planes<CF>(a.boards + b * CF::N, P);
+        FullMT mt;
+        mt.init(a.seeds[b], 0u);
+        apply_and_emit<CF>(P, a, b, mt);
+        uint8_t tmp[CF::N];
+        planes_to_bytes<CF>(P, tmp);
+        for (int x = 0; x < CF::N; ++x) a.out_boards[b * CF::N + x] = (int8_t)tmp[x];
+    }
+}
+
+struct InitArgs {
+    int64_t n;
+    const uint32_t* seeds;       // stateless: seeds[i]; env: seeds[b] (+stride when autoreset)
+    const uint32_t* list;        // nullable: board index list (env autoreset)
+    const uint32_t* list_count;  // nullable: device count for list
+    uint32_t stride;             // env autoreset seed increment (0 = keep seeds)
+    uint32_t* seeds_out;         // nullable: env seed table to update
+    int8_t* boards;
+    uint32_t* draws;         // nullable
+    int32_t* first_action;   // nullable
+    uint32_t* legal;         // nullable
+    uint32_t* mt397;         // nullable
+    int32_t* score;          // nullable (env)
+    int32_t* moves;          // nullable (env)
+    int32_t* reward;         // nullable (env: zeroed on explicit reset)
+    uint8_t* done;           // nullable
+    uint8_t* trunc;          // nullable
+    uint32_t* flags;         // nullable
+};
+
+// BoardV2.__init__ (boardv2.py:17-27) + first seeded random action
+// (samplerTasks.py:11-13). Grid-strided over n (or *list_count).
+template <class CF>
+__global__ void __launch_bounds__(BLOCK) k_init(InitArgs a) {
+    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = a.list ? (int64_t)a.list[i] : i;
+        uint32_t seed = a.seeds[b] + a.stride;
+        if (a.seeds_out) a.seeds_out[b] = seed;
+        FullMT mt;
+        mt.init(seed, 0u);
+        const uint32_t m397 = mt.key[397];
+        typename CF::Bd P[CF::NP];
+        init_board<CF>(P, mt);
+        if (a.draws) a.draws[b] = mt.k;
+        typename CF::Bd HL, VL;
+        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
+        uint32_t act[CF::AW];
+        action_bits<CF>(HL, VL, act);
+        ChainMT rng;  // np.random.seed(cfg.seed) after init (samplerTasks.py:11)
+        rng.init(seed, m397);
+        const int fa = random_action<CF>(act, rng);
+        if (a.first_action) a.first_action[b] = fa;
+        if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
+        if (a.mt397) a.mt397[b] = m397;
+        if (a.score) a.score[b] = 0;
+        if (a.moves) a.moves[b] = 0;
+        if (a.reward) a.reward[b] = 0;
+        if (a.done) a.done[b] = 0;
+        if (a.trunc) a.trunc[b] = 0;
+        if (a.flags) a.flags[b] = fa < 0 ? FLAG_NO_LEGAL : 0u;
+        uint8_t tmp[CF::N];
+        planes_to_bytes<CF>(P, tmp);
+        int8_t* dst = a.boards + b * CF::N;
+        for (int x = 0; x < CF::N; ++x) dst[x] = (int8_t)tmp[x];
+    }
+}
+
+template <class CF>
+__global__ void __launch_bounds__(BLOCK) k_legal(int64_t n, const int8_t* boards, uint32_t* legal) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BLOCK * CF::N + 16];
+    const int64_t b0 = (int64_t)blockIdx.x * BLOCK;
+    const int nb = (int)((n - b0) < BLOCK ? (n - b0) : BLOCK);
+    block_copy_in<CF::N>(boards + b0 * CF::N, lds, nb);
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < nb) {
+        typename CF::Bd P[CF::NP], HL, VL;
+        lds_to_planes<CF>(lds, t, P);
+        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
+        uint32_t act[CF::AW];
+        action_bits<CF>(HL, VL, act);
+        store_legal<CF>(legal + (b0 + t) * CF::AW, act);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// batched env (n x Match3Env, env.py:8-65)
+// ---------------------------------------------------------------------------
+struct EnvArgs {
+    int64_t n;
+    int num_moves, goal;
+    int autoreset;
+    const int8_t* cur;
+    int8_t* nxt;
+    const int32_t* actions;  // nullable -> next_action
+    uint32_t* seeds;
+    uint32_t* mt397;
+    int32_t* score;
+    int32_t* moves;
+    int32_t* next_action;
+    int32_t* reward;
+    uint8_t* done;
+    uint8_t* trunc;
+    uint32_t* flags;
+    uint32_t* draws;
+    uint32_t* legal;  // nullable
+    int32_t* packed;  // nullable: reward<<2 | trunc<<1 | done for the RCCL gather
+    uint32_t* counters;  // [0] overflow count, [1] reset count
+    uint32_t* ovf_list;
+    uint32_t* reset_list;
+};
+
+// Match3Env.step bookkeeping (env.py:48-56) around BoardV2.apply_action.
+template <class CF, class RNG>
+__device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng) {
+    const int act_in = a.actions ? a.actions[b] : a.next_action[b];
+    const int mv = a.moves[b];
+    typename CF::Bd HL, VL;
+    uint32_t f;
+    const int r = apply_action<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL);
+    if (f & FLAG_RNG_OVERFLOW) return false;
+    const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
+    const int sc = a.score[b] + r;
+    const int mv1 = mv + 1;
+    const int tr = sc >= a.goal;                        // env.py:53
+    const int dn = tr || mv1 == a.num_moves;            // env.py:54
+    a.draws[b] = stepped ? rng.k : 0u;
+    uint32_t act[CF::AW];
+    action_bits<CF>(HL, VL, act);
+    int na = -1;
+    if (stepped) {
+        na = random_action<CF>(act, rng);
+        if (na < 0) f |= FLAG_NO_LEGAL;
+    }
+    a.score[b] = sc;
+    a.moves[b] = mv1;
+    a.reward[b] = r;
+    a.trunc[b] = (uint8_t)tr;
+    a.done[b] = (uint8_t)dn;
+    a.flags[b] = f;
+    a.next_action[b] = na;
+    if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
+    if (a.packed) a.packed[b] = (r << 2) | (tr << 1) | dn;
+    if (dn && a.autoreset) {
+        const uint32_t slot = atomicAdd(&a.counters[1], 1u);
+        a.reset_list[slot] = (uint32_t)b;
+    }
+    return true;
+}
+
+template <class CF>
+__global__ void __launch_bounds__(BLOCK) k_env_step(EnvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BLOCK * CF::N + 16];
+    const int64_t b0 = (int64_t)blockIdx.x * BLOCK;
+    const int nb = (int)((a.n - b0) < BLOCK ? (a.n - b0) : BLOCK);
+    block_copy_in<CF::N>(a.cur + b0 * CF::N, lds, nb);
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < nb) {
+        const int64_t b = b0 + t;
+        typename CF::Bd P[CF::NP];
+        lds_to_planes<CF>(lds, t, P);
+        ChainMT rng;
+        rng.init(a.seeds[b], a.mt397[b]);
+        if (!env_step_one<CF>(P, a, b, rng)) {
+            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+            a.ovf_list[slot] = (uint32_t)b;
+        }
+        planes_to_bytes<CF>(P, lds + t * CF::N);
+    }
+    __syncthreads();
+    block_copy_out<CF::N>(a.nxt + b0 * CF::N, lds, nb);
+}
+
+template <class CF>
+__global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
+    const uint32_t cnt = a.counters[0];
+    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
+        const int64_t b = a.ovf_list[i];
+        typename CF::Bd P[CF::NP];
+        bytes_to_planes<CF>(a.cur + b * CF::N, P);
+        FullMT mt;
+        mt.init(a.seeds[b], 0u);
+        env_step_one<CF>(P, a, b, mt);
+        uint8_t tmp[CF::N];
+        planes_to_bytes<CF>(P, tmp);
+        for (int x = 0; x < CF::N; ++x) a.nxt[b * CF::N + x] = (int8_t)tmp[x];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// shape dispatch
+// ---------------------------------------------------------------------------
+#define M3_SHAPES(X) \
+    X(9, 9, 6)       \
+    X(16, 16, 8)
+
+int shape_id(int r, int c, int t) {
+    int id = 0;
+#define X(R_, C_, T_)                                 \
+    if (r == R_ && c == C_ && t == T_) return id; \
+    ++id;
+    M3_SHAPES(X)
+#undef X
+    return -1;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct m3_ctx {
+    int device = 0;
+    int R = 0, C = 0, T = 0, N = 0, A = 0, AW = 0;
+    int shape = -1;
+    hipStream_t stream = nullptr;
+    // stateless scratch
+    void* dbuf = nullptr;
+    size_t dcap = 0;
+    uint32_t* counters = nullptr;  // [0] overflow count
+};
+
+struct m3_env {
+    m3_ctx* ctx = nullptr;
+    int64_t n = 0;
+    int num_moves = 20, goal = 500;
+    int autoreset = 0;
+    uint32_t stride = 0;
+    bool ready = false;
+    int8_t* boards[2] = {nullptr, nullptr};
+    int cur = 0;
+    uint32_t *seeds = nullptr, *mt397 = nullptr, *flags = nullptr, *draws = nullptr, *legal = nullptr;
+    int32_t *score = nullptr, *moves = nullptr, *next_action = nullptr, *reward = nullptr;
+    uint8_t *done = nullptr, *trunc = nullptr;
+    int32_t* actions = nullptr;
+    uint32_t* counters = nullptr;
+    uint32_t *ovf_list = nullptr, *reset_list = nullptr;
+    int32_t* packed = nullptr;
+    int32_t* gathered = nullptr;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    // per-step kernel timing ring (bench.py roofline): event pair i brackets
+    // the i-th k_env_step launch since m3_env_timing(enable)
+    std::vector<hipEvent_t> tev;
+    int tcap = 0, tn = 0;
+};
+
+namespace {
+
+int ensure_scratch(m3_ctx* c, size_t bytes) {
+    if (c->dcap >= bytes) return M3_OK;
+    if (c->dbuf) HIP_TRY(hipFree(c->dbuf));
+    c->dbuf = nullptr;
+    c->dcap = 0;
+    HIP_TRY(hipMalloc(&c->dbuf, bytes));
+    c->dcap = bytes;
+    return M3_OK;
+}
+
+struct Carve {
+    char* base;
+    size_t off = 0;
+    template <class T>
+    T* take(size_t count) {
+        off = (off + 255) & ~size_t(255);
+        T* p = reinterpret_cast<T*>(base + off);
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+size_t carve_size(std::initializer_list<size_t> sizes) {
+    size_t s = 0;
+    for (size_t v : sizes) s = ((s + 255) & ~size_t(255)) + v;
+    return s + 256;
+}
+
+int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
+
+template <class CF>
+int launch_apply(m3_ctx* c, const ApplyArgs& a) {
+    if (a.n == 0) return M3_OK;
+    HIP_TRY(hipMemsetAsync(a.ovf_count, 0, sizeof(uint32_t), c->stream));
+    hipLaunchKernelGGL(k_apply<CF>, dim3(grid_for(a.n)), dim3(BLOCK), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_apply_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    return M3_OK;
+}
+
+template <class CF>
+int launch_init(m3_ctx* c, const InitArgs& a, int64_t max_items) {
+    if (max_items == 0) return M3_OK;
+    int64_t g = grid_for(max_items);
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(BLOCK), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    return M3_OK;
+}
+
+template <class CF>
+int launch_legal(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* legal) {
+    if (n == 0) return M3_OK;
+    hipLaunchKernelGGL(k_legal<CF>, dim3(grid_for(n)), dim3(BLOCK), 0, c->stream, n, boards, legal);
+    HIP_TRY(hipGetLastError());
+    return M3_OK;
+}
+
+template <class CF>
+int launch_env_step(m3_env* e, const int32_t* d_actions) {
+    m3_ctx* c = e->ctx;
+    EnvArgs a;
+    a.n = e->n;
+    a.num_moves = e->num_moves;
+    a.goal = e->goal;
+    a.autoreset = e->autoreset;
+    a.cur = e->boards[e->cur];
+    a.nxt = e->boards[e->cur ^ 1];
+    a.actions = d_actions;
+    a.seeds = e->seeds;
+    a.mt397 = e->mt397;
+    a.score = e->score;
+    a.moves = e->moves;
+    a.next_action = e->next_action;
+    a.reward = e->reward;
+    a.done = e->done;
+    a.trunc = e->trunc;
+    a.flags = e->flags;
+    a.draws = e->draws;
+    a.legal = e->legal;
+    a.packed = e->packed;
+    a.counters = e->counters;
+    a.ovf_list = e->ovf_list;
+    a.reset_list = e->reset_list;
+    HIP_TRY(hipMemsetAsync(e->counters, 0, 2 * sizeof(uint32_t), c->stream));
+    const bool timed = e->tn < e->tcap;
+    if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], c->stream));
+    hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for(e->n)), dim3(BLOCK), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    if (timed) {
+        HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], c->stream));
+        e->tn++;
+    }
+    hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    e->cur ^= 1;
+    if (e->autoreset) {
+        InitArgs r{};
+        r.n = e->n;
+        r.seeds = e->seeds;
+        r.list = e->reset_list;
+        r.list_count = &e->counters[1];
+        r.stride = e->stride;
+        r.seeds_out = e->seeds;
+        r.boards = e->boards[e->cur];
+        r.first_action = e->next_action;
+        r.legal = e->legal;
+        r.mt397 = e->mt397;
+        r.score = e->score;
+        r.moves = e->moves;
+        // reward/done/trunc/flags of the finished step stay visible
+        int rc = launch_init<CF>(c, r, e->n);
+        if (rc) return rc;
+    }
+    return M3_OK;
+}
+
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+template <class F>
+static int with_shape(int shape, F&& f) {
+    int id = 0;
+#define X(R_, C_, T_)                                 \
+    if (shape == id) return f(Cfg<R_, C_, T_>{}); \
+    ++id;
+    M3_SHAPES(X)
+#undef X
+    return set_err(M3_ERR_UNSUPPORTED, "board shape not compiled in");
+}
+
+extern "C" {
+
+int m3_abi_version(void) { return M3_ABI_VERSION; }
+
+const char* m3_last_error(void) { return g_err.c_str(); }
+
+int m3_device_count(int* out) {
+    CHECK_ARG(out, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *out = (e == hipSuccess) ? n : 0;
+    return M3_OK;
+}
+
+int m3_supported(int rows, int columns, int types) { return shape_id(rows, columns, types) >= 0 ? 1 : 0; }
+
+int m3_action_space(int rows, int columns, int* out_actions, int* out_words) {
+    CHECK_ARG(rows > 0 && columns > 0, "bad shape");
+    const int A = rows * (columns - 1) * 2;
+    if (out_actions) *out_actions = A;
+    if (out_words) *out_words = (A + 31) / 32;
+    return M3_OK;
+}
+
+int m3_ctx_create(int device, int rows, int columns, int types, m3_ctx** out) {
+    CHECK_ARG(out, "null out");
+    *out = nullptr;
+    const int sid = shape_id(rows, columns, types);
+    if (sid < 0)
+        return set_err(M3_ERR_UNSUPPORTED, "BoardConfig(rows=%d, columns=%d, types=%d) is not compiled in", rows,
+                       columns, types);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return set_err(M3_ERR_NO_DEVICE, "no HIP device visible (libm3 has no CPU fallback)");
+    CHECK_ARG(device >= 0 && device < ndev, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_err(M3_ERR_NO_DEVICE, "device %d is %s; libm3 is built for gfx950 only", device, prop.gcnArchName);
+    m3_ctx* c = new m3_ctx;
+    c->device = device;
+    c->R = rows;
+    c->C = columns;
+    c->T = types;
+    c->N = rows * columns;
+    c->A = rows * (columns - 1) * 2;
+    c->AW = (c->A + 31) / 32;
+    c->shape = sid;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->counters, 256);
+    if (e != hipSuccess) {
+        delete c;
+        return set_err(M3_ERR_HIP, "context setup: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return M3_OK;
+}
+
+int m3_ctx_destroy(m3_ctx* c) {
+    if (!c) return M3_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->dbuf) (void)hipFree(c->dbuf);
+    if (c->counters) (void)hipFree(c->counters);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return M3_OK;
+}
+
+int m3_ctx_synchronize(m3_ctx* c) {
+    CHECK_ARG(c, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return M3_OK;
+}
+
+int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boards, uint32_t* out_draws,
+                   int32_t* out_first_action) {
+    CHECK_ARG(c && n >= 0 && (n == 0 || (seeds && out_boards)), "bad arguments");
+    if (n == 0) return M3_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t need = carve_size({n * 4ull, n * (size_t)c->N, n * 4ull, n * 4ull});
+    int rc = ensure_scratch(c, need);
+    if (rc) return rc;
+    Carve cv{(char*)c->dbuf};
+    uint32_t* d_seeds = cv.take<uint32_t>(n);
+    int8_t* d_boards = cv.take<int8_t>(n * c->N);
+    uint32_t* d_draws = cv.take<uint32_t>(n);
+    int32_t* d_first = cv.take<int32_t>(n);
+    HIP_TRY(hipMemcpyAsync(d_seeds, seeds, n * 4, hipMemcpyHostToDevice, c->stream));
+    InitArgs a{};
+    a.n = n;
+    a.seeds = d_seeds;
+    a.boards = d_boards;
+    a.draws = d_draws;
+    a.first_action = d_first;
+    rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c, a, n); });
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out_boards, d_boards, n * c->N, hipMemcpyDeviceToHost, c->stream));
+    if (out_draws) HIP_TRY(hipMemcpyAsync(out_draws, d_draws, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (out_first_action) HIP_TRY(hipMemcpyAsync(out_first_action, d_first, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return M3_OK;
+}
+
+int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seeds, const int32_t* n_actions,
+                     const int32_t* actions, int8_t* out_boards, int32_t* out_reward, uint32_t* out_draws,
+                     uint32_t* out_flags, uint32_t* out_legal_bits, int32_t* out_next_action) {
+    CHECK_ARG(c && n >= 0, "bad arguments");
+    if (n == 0) return M3_OK;
+    CHECK_ARG(boards && seeds && n_actions && actions && out_boards && out_reward && out_draws && out_flags,
+              "null buffer");
+    for (int64_t i = 0; i < n * c->N; ++i)
+        if (boards[i] < 0) return set_err(M3_ERR_INVALID, "cell value outside [0, 127] at byte %lld", (long long)i);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = n * (size_t)c->N;
+    const size_t need = carve_size({bytes, n * 4ull, n * 4ull, n * 4ull, bytes, n * 4ull, n * 4ull, n * 4ull,
+                                    n * 4ull * c->AW, n * 4ull, n * 4ull});
+    int rc = ensure_scratch(c, need);
+    if (rc) return rc;
+    Carve cv{(char*)c->dbuf};
+    ApplyArgs a{};
+    a.n = n;
+    int8_t* d_in = cv.take<int8_t>(bytes);
+    uint32_t* d_seeds = cv.take<uint32_t>(n);
+    int32_t* d_na = cv.take<int32_t>(n);
+    int32_t* d_act = cv.take<int32_t>(n);
+    a.boards = d_in;
+    a.seeds = d_seeds;
+    a.n_actions = d_na;
+    a.actions = d_act;
+    a.out_boards = cv.take<int8_t>(bytes);
+    a.reward = cv.take<int32_t>(n);
+    a.draws = cv.take<uint32_t>(n);
+    a.flags = cv.take<uint32_t>(n);
+    a.legal = out_legal_bits ? cv.take<uint32_t>(n * c->AW) : nullptr;
+    a.next_action = out_next_action ? cv.take<int32_t>(n) : nullptr;
+    a.ovf_list = cv.take<uint32_t>(n);
+    a.ovf_count = c->counters;
+    HIP_TRY(hipMemcpyAsync(d_in, boards, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_seeds, seeds, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_na, n_actions, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_act, actions, n * 4, hipMemcpyHostToDevice, c->stream));
+    rc = with_shape(c->shape, [&](auto cf) { return launch_apply<decltype(cf)>(c, a); });
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out_boards, a.out_boards, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_reward, a.reward, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_draws, a.draws, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_flags, a.flags, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (out_legal_bits)
+        HIP_TRY(hipMemcpyAsync(out_legal_bits, a.legal, n * 4ull * c->AW, hipMemcpyDeviceToHost, c->stream));
+    if (out_next_action)
+        HIP_TRY(hipMemcpyAsync(out_next_action, a.next_action, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return M3_OK;
+}
+
+int m3_legal_actions(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* out_legal_bits) {
+    CHECK_ARG(c && n >= 0, "bad arguments");
+    if (n == 0) return M3_OK;
+    CHECK_ARG(boards && out_legal_bits, "null buffer");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = n * (size_t)c->N;
+    int rc = ensure_scratch(c, carve_size({bytes, n * 4ull * c->AW}));
+    if (rc) return rc;
+    Carve cv{(char*)c->dbuf};
+    int8_t* d_in = cv.take<int8_t>(bytes);
+    uint32_t* d_out = cv.take<uint32_t>(n * c->AW);
+    HIP_TRY(hipMemcpyAsync(d_in, boards, bytes, hipMemcpyHostToDevice, c->stream));
+    rc = with_shape(c->shape, [&](auto cf) { return launch_legal<decltype(cf)>(c, n, d_in, d_out); });
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out_legal_bits, d_out, n * 4ull * c->AW, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return M3_OK;
+}
+
+// ---- env ------------------------------------------------------------------
+int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** out) {
+    CHECK_ARG(c && out && n > 0 && num_moves > 0, "bad arguments");
+    CHECK_ARG(n < (int64_t)1 << 31, "n too large");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(c->device));
+    m3_env* e = new m3_env;
+    e->ctx = c;
+    e->n = n;
+    e->num_moves = num_moves;
+    e->goal = env_goal;
+    const size_t bytes = n * (size_t)c->N;
+    hipError_t err = hipSuccess;
+    auto alloc = [&](auto** p, size_t sz) {
+        if (err == hipSuccess) err = hipMalloc((void**)p, sz ? sz : 4);
+    };
+    alloc(&e->boards[0], bytes);
+    alloc(&e->boards[1], bytes);
+    alloc(&e->seeds, n * 4);
+    alloc(&e->mt397, n * 4);
+    alloc(&e->flags, n * 4);
+    alloc(&e->draws, n * 4);
+    alloc(&e->legal, n * 4ull * c->AW);
+    alloc(&e->score, n * 4);
+    alloc(&e->moves, n * 4);
+    alloc(&e->next_action, n * 4);
+    alloc(&e->reward, n * 4);
+    alloc(&e->done, n);
+    alloc(&e->trunc, n);
+    alloc(&e->actions, n * 4);
+    alloc(&e->counters, 256);
+    alloc(&e->ovf_list, n * 4);
+    alloc(&e->reset_list, n * 4);
+    alloc(&e->packed, n * 4);
+    if (err != hipSuccess) {
+        m3_env_destroy(e);
+        return set_err(M3_ERR_HIP, "env allocation (%lld boards): %s", (long long)n, hipGetErrorString(err));
+    }
+    *out = e;
+    return M3_OK;
+}
+
+int m3_env_destroy(m3_env* e) {
+    if (!e) return M3_OK;
+    (void)hipSetDevice(e->ctx->device);
+    (void)hipStreamSynchronize(e->ctx->stream);
+    void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->mt397, e->flags, e->draws, e->legal,
+                    e->score, e->moves, e->next_action, e->reward, e->done, e->trunc, e->actions,
+                    e->counters, e->ovf_list, e->reset_list, e->packed, e->gathered};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (e->comm) ncclCommDestroy(e->comm);
+    for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
+    delete e;
+    return M3_OK;
+}
+
+int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
+    CHECK_ARG(e, "null env");
+    m3_ctx* c = e->ctx;
+    HIP_TRY(hipSetDevice(c->device));
+    if (seeds) {
+        HIP_TRY(hipMemcpyAsync(e->seeds, seeds, e->n * 4, hipMemcpyHostToDevice, c->stream));
+    } else {
+        // seeds = seed_base + i, written on host once (reset is not on the hot path)
+        uint32_t* h = (uint32_t*)malloc(e->n * 4);
+        if (!h) return set_err(M3_ERR_INVALID, "host allocation failed");
+        for (int64_t i = 0; i < e->n; ++i) h[i] = seed_base + (uint32_t)i;
+        hipError_t err = hipMemcpy(e->seeds, h, e->n * 4, hipMemcpyHostToDevice);
+        free(h);
+        HIP_TRY(err);
+    }
+    InitArgs a{};
+    a.n = e->n;
+    a.seeds = e->seeds;
+    a.boards = e->boards[e->cur];
+    a.first_action = e->next_action;
+    a.legal = e->legal;
+    a.mt397 = e->mt397;
+    a.score = e->score;
+    a.moves = e->moves;
+    a.reward = e->reward;
+    a.done = e->done;
+    a.trunc = e->trunc;
+    a.flags = e->flags;
+    a.draws = e->draws;
+    int rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c, a, e->n); });
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    e->ready = true;
+    return M3_OK;
+}
+
+int m3_env_set_autoreset(m3_env* e, int enabled, uint32_t seed_stride) {
+    CHECK_ARG(e, "null env");
+    e->autoreset = enabled ? 1 : 0;
+    e->stride = seed_stride;
+    return M3_OK;
+}
+
+int m3_env_step_device(m3_env* e, const int32_t* d_actions) {
+    CHECK_ARG(e, "null env");
+    if (!e->ready) return set_err(M3_ERR_STATE, "m3_env_step before m3_env_reset");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    return with_shape(e->ctx->shape, [&](auto cf) { return launch_env_step<decltype(cf)>(e, d_actions); });
+}
+
+int m3_env_step(m3_env* e, const int32_t* actions) {
+    CHECK_ARG(e, "null env");
+    if (actions) {
+        HIP_TRY(hipSetDevice(e->ctx->device));
+        HIP_TRY(hipMemcpyAsync(e->actions, actions, e->n * 4, hipMemcpyHostToDevice, e->ctx->stream));
+        return m3_env_step_device(e, e->actions);
+    }
+    return m3_env_step_device(e, nullptr);
+}
+
+static int env_field(m3_env* e, int what, void** ptr, size_t* bytes) {
+    const int64_t n = e->n;
+    switch (what) {
+        case M3_ENV_BOARDS: *ptr = e->boards[e->cur]; *bytes = n * (size_t)e->ctx->N; return M3_OK;
+        case M3_ENV_REWARD: *ptr = e->reward; *bytes = n * 4; return M3_OK;
+        case M3_ENV_DONE: *ptr = e->done; *bytes = n; return M3_OK;
+        case M3_ENV_TRUNCATED: *ptr = e->trunc; *bytes = n; return M3_OK;
+        case M3_ENV_SCORE: *ptr = e->score; *bytes = n * 4; return M3_OK;
+        case M3_ENV_MOVES: *ptr = e->moves; *bytes = n * 4; return M3_OK;
+        case M3_ENV_FLAGS: *ptr = e->flags; *bytes = n * 4; return M3_OK;
+        case M3_ENV_NEXT_ACTION: *ptr = e->next_action; *bytes = n * 4; return M3_OK;
+        case M3_ENV_LEGAL: *ptr = e->legal; *bytes = n * 4ull * e->ctx->AW; return M3_OK;
+        case M3_ENV_SEEDS: *ptr = e->seeds; *bytes = n * 4; return M3_OK;
+        case M3_ENV_DRAWS: *ptr = e->draws; *bytes = n * 4; return M3_OK;
+        default: return set_err(M3_ERR_INVALID, "unknown env field %d", what);
+    }
+}
+
+int m3_env_get(m3_env* e, int what, void* host_out) {
+    CHECK_ARG(e && host_out, "bad arguments");
+    void* p;
+    size_t bytes;
+    int rc = env_field(e, what, &p, &bytes);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    HIP_TRY(hipMemcpyAsync(host_out, p, bytes, hipMemcpyDeviceToHost, e->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(e->ctx->stream));
+    return M3_OK;
+}
+
+int m3_env_device_ptr(m3_env* e, int what, void** out) {
+    CHECK_ARG(e && out, "bad arguments");
+    size_t bytes;
+    return env_field(e, what, out, &bytes);
+}
+
+int m3_comm_unique_id(uint8_t out_id[128]) {
+    CHECK_ARG(out_id, "null out");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    RCCL_TRY(ncclGetUniqueId(&id));
+    memcpy(out_id, &id, 128);
+    return M3_OK;
+}
+
+int m3_env_comm_init(m3_env* e, const uint8_t id[128], int nranks, int rank) {
+    CHECK_ARG(e && id && nranks >= 1 && rank >= 0 && rank < nranks, "bad arguments");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    ncclUniqueId uid;
+    memcpy(&uid, id, 128);
+    RCCL_TRY(ncclCommInitRank(&e->comm, nranks, uid, rank));
+    e->nranks = nranks;
+    e->rank = rank;
+    HIP_TRY(hipMalloc(&e->gathered, (size_t)nranks * e->n * 4));
+    return M3_OK;
+}
+
+int m3_env_gather(m3_env* e, int32_t* host_out) {
+    CHECK_ARG(e, "null env");
+    if (!e->comm) return set_err(M3_ERR_STATE, "m3_env_gather before m3_env_comm_init");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    RCCL_TRY(ncclAllGather(e->packed, e->gathered, (size_t)e->n, ncclInt32, e->comm, e->ctx->stream));
+    if (host_out) {
+        HIP_TRY(hipMemcpyAsync(host_out, e->gathered, (size_t)e->nranks * e->n * 4, hipMemcpyDeviceToHost,
+                               e->ctx->stream));
+        HIP_TRY(hipStreamSynchronize(e->ctx->stream));
+    }
+    return M3_OK;
+}
+
+int m3_env_timing(m3_env* e, int capacity) {
+    CHECK_ARG(e && capacity >= 0, "bad arguments");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    HIP_TRY(hipStreamSynchronize(e->ctx->stream));
+    while ((int)e->tev.size() < 2 * capacity) {
+        hipEvent_t ev;
+        HIP_TRY(hipEventCreate(&ev));
+        e->tev.push_back(ev);
+    }
+    e->tcap = capacity;
+    e->tn = 0;
+    return M3_OK;
+}
+
+int m3_env_kernel_ms(m3_env* e, float* out_ms, int max_n, int* out_n) {
+    CHECK_ARG(e && out_n && (max_n == 0 || out_ms), "bad arguments");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    const int n = e->tn < max_n ? e->tn : max_n;
+    if (n > 0) HIP_TRY(hipEventSynchronize(e->tev[2 * (n - 1) + 1]));
+    for (int i = 0; i < n; ++i) HIP_TRY(hipEventElapsedTime(&out_ms[i], e->tev[2 * i], e->tev[2 * i + 1]));
+    *out_n = n;
+    return M3_OK;
+}
+
+}  // extern "C"

@@ -188,7 +188,7 @@ M3_HD void action_bits_rows(const typename CF::Bd& HL, const typename CF::Bd& VL
         const uint32_t f = h | (v << (C - 1));  // 2C-1 <= 31 bits
         constexpr int q = POS >> 5, s = POS & 31;
         act[q] |= f << s;
-        if constexpr (s != 0 && s + 2 * C - 1 > 32) act[q + 1] |= f >> (32 - s);
+        if constexpr (s != 0 && s + 2 * C - 1 > 32 && q + 1 < CF::AW) act[q + 1] |= f >> (32 - s);
         action_bits_rows<CF, ROW + 1>(HL, VL, act);
     }
 }
@@ -576,7 +576,7 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
                        typename CF::Bd& HL, typename CF::Bd& VL) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
-    constexpr int C = CF::C, R = CF::R, BITS = CF::BITS, TM = CF::TM;
+    constexpr int C = CF::C, R = CF::R, TM = CF::TM;
     constexpr int H = CF::H, V = CF::V, B = CF::B, M = CF::M;
     constexpr Bd VALID = G::valid();
     flags = 0u;

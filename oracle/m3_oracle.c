@@ -560,6 +560,21 @@ int m3o_random_episode(const m3o_cfg *cfg, uint32_t seed, int num_moves, int env
     return moves;
 }
 
+/* n independent seeded episodes, all per-move outputs kept (parity checks). */
+void m3o_batch_episodes(const m3o_cfg *cfg, int64_t n, const uint32_t *seeds, int num_moves, int env_goal,
+                        int nthreads, int32_t *actions, int32_t *rewards, int32_t *draws, uint8_t *done,
+                        int32_t *final_boards, int32_t *moves_out, int32_t *flags_out) {
+    const int N = cfg->R * cfg->C;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 16)
+    for (int64_t i = 0; i < n; i++) {
+        int f = 0;
+        moves_out[i] = m3o_random_episode(cfg, seeds[i], num_moves, env_goal, actions + i * num_moves,
+                                          rewards + i * num_moves, draws + i * num_moves, done + i * num_moves,
+                                          final_boards + i * N, &f);
+        flags_out[i] = f;
+    }
+}
+
 int64_t m3o_run_episodes(const m3o_cfg *cfg, int64_t n, const uint32_t *seeds,
                          int num_moves, int env_goal, int nthreads, int64_t *out_total) {
     int64_t steps = 0;

@@ -75,6 +75,12 @@ int m3o_random_episode(const m3o_cfg *cfg, uint32_t seed, int num_moves, int env
                        int32_t *actions, int32_t *rewards, int32_t *draws,
                        uint8_t *done, int32_t *final_board, int *flags);
 
+/* Threaded: n seeded episodes with every per-move output kept
+ * (actions/rewards/draws/done are [n][num_moves], final_boards [n][R*C]). */
+void m3o_batch_episodes(const m3o_cfg *cfg, int64_t n, const uint32_t *seeds, int num_moves, int env_goal,
+                        int nthreads, int32_t *actions, int32_t *rewards, int32_t *draws, uint8_t *done,
+                        int32_t *final_boards, int32_t *moves_out, int32_t *flags_out);
+
 /* Threaded CPU baseline: run n episodes (seeds[i]) of num_moves moves with
  * random actions; returns total env steps; writes per-episode total reward. */
 int64_t m3o_run_episodes(const m3o_cfg *cfg, int64_t n, const uint32_t *seeds,

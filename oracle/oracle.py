@@ -43,7 +43,10 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+        srcs = [os.path.join(_HERE, f) for f in ("m3_oracle.c", "m3_oracle.h")]
+        if not os.path.exists(_LIB_PATH) or (
+                all(os.path.exists(s) for s in srcs)
+                and os.path.getmtime(_LIB_PATH) < max(os.path.getmtime(s) for s in srcs)):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         P = ctypes.POINTER
@@ -76,6 +79,9 @@ def lib():
         L.m3o_run_episodes.argtypes = [P(Cfg), ctypes.c_int64, u32p, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, i64p]
         L.m3o_run_episodes.restype = ctypes.c_int64
+        L.m3o_batch_episodes.argtypes = [P(Cfg), ctypes.c_int64, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         i32p, i32p, i32p, u8p, i32p, i32p, i32p]
+        L.m3o_batch_episodes.restype = None
         _lib = L
     return _lib
 
@@ -150,6 +156,24 @@ class Oracle:
                                      _p(done, ctypes.c_uint8), _p(fb, ctypes.c_int32), ctypes.byref(flags))
         return dict(n=n, actions=acts[:n], rewards=rews[:n], draws=drw[:n], done=done[:n],
                     final=fb, flags=int(flags.value))
+
+    def batch_episodes(self, seeds, num_moves=20, env_goal=2**31 - 1, threads=None):
+        """Seeded random episodes for many boards at once (OpenMP over boards)."""
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        n = len(seeds)
+        threads = threads or min(16, os.cpu_count() or 1)
+        acts = np.zeros((n, num_moves), np.int32)
+        rews = np.zeros((n, num_moves), np.int32)
+        drw = np.zeros((n, num_moves), np.int32)
+        done = np.zeros((n, num_moves), np.uint8)
+        final = np.zeros((n, self.R * self.C), np.int32)
+        moves = np.zeros(n, np.int32)
+        flags = np.zeros(n, np.int32)
+        lib().m3o_batch_episodes(ctypes.byref(self.cfg), n, _p(seeds, ctypes.c_uint32), num_moves, env_goal, threads,
+                                 _p(acts, ctypes.c_int32), _p(rews, ctypes.c_int32), _p(drw, ctypes.c_int32),
+                                 _p(done, ctypes.c_uint8), _p(final, ctypes.c_int32), _p(moves, ctypes.c_int32),
+                                 _p(flags, ctypes.c_int32))
+        return dict(actions=acts, rewards=rews, draws=drw, done=done, final=final, moves=moves, flags=flags)
 
     def run_episodes(self, seeds, num_moves=20, env_goal=2**31 - 1, threads=1):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint32)

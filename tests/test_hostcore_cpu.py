@@ -1,0 +1,87 @@
+"""The device rule code (m3_rules.hpp), compiled for the HOST by a test-only harness
+(tests/hostcore), differential-tested against the reference fixtures and the oracle.
+This checks the bitboard logic without a GPU; the HIP path itself is covered by the
+-m gpu tests."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, SHAPES
+from oracle import Oracle
+
+sys.path.insert(0, os.path.join(ROOT, "tests", "hostcore"))
+from hostcore import HostCore, lib  # noqa: E402
+
+
+def test_chain_mt_matches_numpy_stream(golden):
+    g = golden("prng")
+    for s, r in zip(g["seeds"], g["raw"]):
+        for k in (0, 1, 226, 227, 453, 454, 622, 623):
+            assert lib().hc_chain_draw(int(s), k) == r[k]
+        assert lib().hc_chain_draw(int(s), 624) == 0xFFFFFFFF  # beyond the first block: overflow
+
+
+@pytest.mark.parametrize("tag", list(SHAPES))
+def test_roundtrip_planes(tag):
+    hc = HostCore(*SHAPES[tag])
+    b = np.random.default_rng(1).integers(0, 128, size=(500, hc.N)).astype(np.int8)
+    assert (hc.roundtrip(b) == b).all()
+
+
+@pytest.mark.parametrize("tag", list(SHAPES))
+def test_matches_legal_init_steps_golden(golden, tag):
+    hc = HostCore(*SHAPES[tag])
+    m = golden("matches")
+    mask, sp, fd = hc.matches(m["tb_" + tag])
+    assert (mask == m["mask_" + tag].reshape(len(mask), -1)).all()
+    assert (sp == m["spawn_" + tag].reshape(len(sp), -1)).all()
+    assert ((fd > 0) == (m["ngroups_" + tag] > 0)).all()
+    lg = golden("legal")
+    bits = np.unpackbits(hc.legal(lg["boards_" + tag]).view(np.uint8), axis=1, bitorder="little")
+    assert (bits[:, :lg["legal_" + tag].shape[1]] == lg["legal_" + tag]).all()
+    ini = golden("init")
+    out, drw, _, _ = hc.init(ini["seeds_" + tag])
+    assert (out == ini["boards_" + tag].reshape(len(out), -1)).all() and (drw == ini["draws_" + tag]).all()
+    st = golden("steps")
+    out, rew, drw, flg, _, _ = hc.apply(st["board_" + tag], st["seed_" + tag], st["n_actions_" + tag],
+                                        st["action_" + tag])
+    assert (out == st["next_" + tag].reshape(len(out), -1)).all()
+    assert (rew == st["reward_" + tag]).all()
+    live = st["draws_" + tag] >= 0
+    assert (drw[live] == st["draws_" + tag][live]).all()
+
+
+@pytest.mark.parametrize("tag", list(SHAPES))
+def test_episodes_golden(golden, tag):
+    hc = HostCore(*SHAPES[tag])
+    e = golden("episodes")
+    seeds = e["seeds_" + tag].astype(np.uint32)
+    b, _, _, act = hc.init(seeds)
+    for m in range(20):
+        assert (act == e["actions_" + tag][:, m]).all()
+        b, rew, drw, _, _, act = hc.apply(b, seeds, 20 - m, act)
+        assert (rew == e["rewards_" + tag][:, m]).all()
+        assert (drw == e["draws_" + tag][:, m]).all()
+    assert (b == e["final_" + tag].reshape(len(b), -1)).all()
+
+
+def test_random_states_vs_oracle():
+    """Boards with random specials/typed values and random (incl. illegal) actions."""
+    rng = np.random.default_rng(11)
+    hc, o = HostCore(), Oracle()
+    n = 3000
+    seeds = rng.integers(1, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    boards, _, _, _ = hc.init(seeds)
+    sprinkle = rng.random((n, 81)) < 0.06
+    vals = rng.choice([8, 16, 24, 32, 11, 19, 27, 40, 56, 0, 127], size=(n, 81))
+    boards = np.where(sprinkle, vals, boards).astype(np.int8)
+    acts = rng.integers(0, 144, size=n)
+    out, rew, drw, flg, legal, nxt = hc.apply(boards, seeds, 20, acts)
+    for i in range(n):
+        ob, orr, od, of = o.apply_action(boards[i].astype(np.int32), int(seeds[i]), int(acts[i]))
+        assert (ob.reshape(-1) == out[i]).all() and orr == rew[i] and od == drw[i], i
+        bits = np.zeros(144, np.uint8)
+        bits[o.legal_actions(ob)] = 1
+        assert (np.unpackbits(legal[i].view(np.uint8), bitorder="little")[:144] == bits).all()
