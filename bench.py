@@ -129,6 +129,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kms = env.kernel_ms()
+    stats = env.stats()
     env.close()
 
     if rank != 0:
@@ -164,7 +165,10 @@ def main():
             "num_moves": args.moves,
             "env_goal": args.goal,
             "parallelism": f"dp{world}",
+            "shards_per_gpu": stats["shards"],
         },
+        "path_stats": {"autoresets": stats["autoresets"], "reset_recomputes": stats["reset_recomputes"],
+                       "step_recomputes": stats["step_recomputes"]},
         "roofline": {
             "bound": "hbm",
             "kernel": "k_env_step",

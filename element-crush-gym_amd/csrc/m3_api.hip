@@ -21,6 +21,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -66,11 +67,52 @@ int set_err(int code, const char* fmt, ...) {
 constexpr int BLOCK = 256;
 constexpr int FIX_BLOCK = 64;
 constexpr int FIX_GRID = 256;
+constexpr int INIT_BLOCK = 64;
+constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
+
+// Per-shape step-kernel geometry: boards (lanes) per workgroup and the
+// match-group table capacity, sized so staging + table fit the 160 KB LDS.
+template <class CF>
+struct KS {
+    static constexpr int B = CF::N > 128 ? 128 : 256;
+    static constexpr int GCAP = CF::N > 128 ? 4 : 8;
+};
+
+// Per-lane match-group table in LDS (see m3_rules.hpp, match_scan). Entry
+// (g, h|v, word i) of lane l lives at tab[((g*2 + hv)*W + i)*LANES + l]:
+// consecutive lanes hit consecutive dwords, so every access is conflict-free.
+template <class CF, int CAP_, int LANES>
+struct LdsStore {
+    static constexpr int CAP = CAP_;
+    static constexpr int W = CF::W;
+    static constexpr int BLOCK = LANES;
+    static constexpr int WORDS = CAP * 2 * W * BLOCK;
+    uint32_t* tab;  // already offset by threadIdx.x
+    __device__ __forceinline__ typename CF::Bd get_h(int g) const {
+        typename CF::Bd r;
+#pragma unroll
+        for (int i = 0; i < W; ++i) r.w[i] = tab[((g * 2) * W + i) * BLOCK];
+        return r;
+    }
+    __device__ __forceinline__ typename CF::Bd get_v(int g) const {
+        typename CF::Bd r;
+#pragma unroll
+        for (int i = 0; i < W; ++i) r.w[i] = tab[((g * 2 + 1) * W + i) * BLOCK];
+        return r;
+    }
+    __device__ __forceinline__ void put(int g, const typename CF::Bd& h, const typename CF::Bd& v) {
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            tab[((g * 2) * W + i) * BLOCK] = h.w[i];
+            tab[((g * 2 + 1) * W + i) * BLOCK] = v.w[i];
+        }
+    }
+};
 
 // ---------------------------------------------------------------------------
 // LDS staging
 // ---------------------------------------------------------------------------
-template <int N>
+template <int N, int BLOCK>
 __device__ __forceinline__ void block_copy_in(const int8_t* __restrict__ g, uint8_t* lds, int nb) {
     const int bytes = nb * N;
     const int n16 = bytes >> 4;
@@ -80,7 +122,7 @@ __device__ __forceinline__ void block_copy_in(const int8_t* __restrict__ g, uint
     for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) lds[i] = (uint8_t)g[i];
 }
 
-template <int N>
+template <int N, int BLOCK>
 __device__ __forceinline__ void block_copy_out(int8_t* __restrict__ g, const uint8_t* lds, int nb) {
     const int bytes = nb * N;
     const int n16 = bytes >> 4;
@@ -163,12 +205,13 @@ struct ApplyArgs {
 };
 
 // one full apply_action + outputs for board b; returns false on RNG overflow
-template <class CF, class RNG>
-__device__ __forceinline__ bool apply_and_emit(typename CF::Bd* P, const ApplyArgs& a, int64_t b, RNG& rng) {
+template <class CF, class RNG, class Store>
+__device__ __forceinline__ bool apply_and_emit(typename CF::Bd* P, const ApplyArgs& a, int64_t b, RNG& rng,
+                                               Store& st) {
     typename CF::Bd HL, VL;
     uint32_t f;
-    const int r = apply_action<CF>(P, a.n_actions[b], a.actions[b], rng, f, HL, VL);
-    if (f & FLAG_RNG_OVERFLOW) return false;
+    const int r = apply_action<CF>(P, a.n_actions[b], a.actions[b], rng, f, HL, VL, st);
+    if (f & FLAG_RECOMPUTE) return false;
     const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
     a.reward[b] = r;
     a.draws[b] = stepped ? rng.k : 0u;
@@ -186,11 +229,12 @@ __device__ __forceinline__ bool apply_and_emit(typename CF::Bd* P, const ApplyAr
 }
 
 template <class CF>
-__global__ void __launch_bounds__(BLOCK) k_apply(ApplyArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BLOCK * CF::N + 16];
-    const int64_t b0 = (int64_t)blockIdx.x * BLOCK;
-    const int nb = (int)((a.n - b0) < BLOCK ? (a.n - b0) : BLOCK);
-    block_copy_in<CF::N>(a.boards + b0 * CF::N, lds, nb);
+__global__ void __launch_bounds__(KS<CF>::B) k_apply(ApplyArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[KS<CF>::B * CF::N + 16];
+    __shared__ uint32_t gtab[LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::WORDS];
+    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
+    const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
+    block_copy_in<CF::N, KS<CF>::B>(a.boards + b0 * CF::N, lds, nb);
     __syncthreads();
     const int t = threadIdx.x;
     if (t < nb) {
@@ -200,14 +244,15 @@ __global__ void __launch_bounds__(BLOCK) k_apply(ApplyArgs a) {
         const uint32_t s = a.seeds[b];
         ChainMT rng;
         rng.init(s, mt_state397(s));
-        if (!apply_and_emit<CF>(P, a, b, rng)) {
+        LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};
+        if (!apply_and_emit<CF>(P, a, b, rng, st)) {
             const uint32_t slot = atomicAdd(a.ovf_count, 1u);
             a.ovf_list[slot] = (uint32_t)b;
         }
         planes_to_bytes<CF>(P, lds + t * CF::N);
     }
     __syncthreads();
-    block_copy_out<CF::N>(a.out_boards + b0 * CF::N, lds, nb);
+    block_copy_out<CF::N, KS<CF>::B>(a.out_boards + b0 * CF::N, lds, nb);
 }
 
 // redo overflowed boards with the full 624-word state (lane-private scratch)
@@ -218,9 +263,11 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.boards + b * CF::N, P);
-        FullMT mt;
+        FullMT mt;  // scratch: this pass almost never has work, and an LDS state would
+                    // make even an empty launch wait for a whole free CU
         mt.init(a.seeds[b], 0u);
-        apply_and_emit<CF>(P, a, b, mt);
+        ArrayStore<CF> st;
+        apply_and_emit<CF>(P, a, b, mt, st);
         uint8_t tmp[CF::N];
         planes_to_bytes<CF>(P, tmp);
         for (int x = 0; x < CF::N; ++x) a.out_boards[b * CF::N + x] = (int8_t)tmp[x];
@@ -245,52 +292,192 @@ struct InitArgs {
     uint8_t* done;           // nullable
     uint8_t* trunc;          // nullable
     uint32_t* flags;         // nullable
+    uint32_t* ovf_count;     // boards whose init needed >= 624 draws (FullMT recompute)
+    uint32_t* ovf_list;
 };
 
 // BoardV2.__init__ (boardv2.py:17-27) + first seeded random action
-// (samplerTasks.py:11-13). Grid-strided over n (or *list_count).
+// (samplerTasks.py:11-13) for board b. Returns false if the stream overflowed.
+// Everything a reset writes besides the cells: legal set, the first seeded
+// random action (np.random.seed(cfg.seed) then choice(legal), samplerTasks.py:11-13),
+// the cached mt[397] and the zeroed episode state.
 template <class CF>
-__global__ void __launch_bounds__(BLOCK) k_init(InitArgs a) {
+__device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, uint32_t seed, uint32_t m397,
+                                             uint32_t draws, const typename CF::Bd* P) {
+    typename CF::Bd HL, VL;
+    legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
+    uint32_t act[CF::AW];
+    action_bits<CF>(HL, VL, act);
+    ChainMT rng;
+    rng.init(seed, m397);
+    const int fa = random_action<CF>(act, rng);
+    if (a.draws) a.draws[b] = draws;
+    if (a.first_action) a.first_action[b] = fa;
+    if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
+    if (a.mt397) a.mt397[b] = m397;
+    if (a.score) a.score[b] = 0;
+    if (a.moves) a.moves[b] = 0;
+    if (a.reward) a.reward[b] = 0;
+    if (a.done) a.done[b] = 0;
+    if (a.trunc) a.trunc[b] = 0;
+    if (a.flags) a.flags[b] = fa < 0 ? FLAG_NO_LEGAL : 0u;
+}
+
+template <class CF, class RNG>
+__device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t m397, RNG& mt) {
+    typename CF::Bd P[CF::NP];
+    init_board<CF>(P, mt);
+    if (mt.overflow) return false;
+    init_outputs<CF>(a, b, seed, m397, mt.k, P);
+    uint8_t tmp[CF::N];
+    planes_to_bytes<CF>(P, tmp);
+    int8_t* dst = a.boards + b * CF::N;
+    for (int x = 0; x < CF::N; ++x) dst[x] = (int8_t)tmp[x];
+    return true;
+}
+
+// Reset on the register-only MT19937 chain; grid-strided over n (or *list_count).
+template <class CF>
+__global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
-    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * BLOCK) {
+    if (a.list_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.ovf_count + 8, (uint32_t)cnt);  // stats: resets
+    for (int64_t i = (int64_t)blockIdx.x * INIT_BLOCK + threadIdx.x; i < cnt;
+         i += (int64_t)gridDim.x * INIT_BLOCK) {
         const int64_t b = a.list ? (int64_t)a.list[i] : i;
-        uint32_t seed = a.seeds[b] + a.stride;
+        const uint32_t seed = a.seeds[b] + a.stride;
         if (a.seeds_out) a.seeds_out[b] = seed;
-        FullMT mt;
-        mt.init(seed, 0u);
-        const uint32_t m397 = mt.key[397];
-        typename CF::Bd P[CF::NP];
-        init_board<CF>(P, mt);
-        if (a.draws) a.draws[b] = mt.k;
-        typename CF::Bd HL, VL;
-        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
-        uint32_t act[CF::AW];
-        action_bits<CF>(HL, VL, act);
-        ChainMT rng;  // np.random.seed(cfg.seed) after init (samplerTasks.py:11)
-        rng.init(seed, m397);
-        const int fa = random_action<CF>(act, rng);
-        if (a.first_action) a.first_action[b] = fa;
-        if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
-        if (a.mt397) a.mt397[b] = m397;
-        if (a.score) a.score[b] = 0;
-        if (a.moves) a.moves[b] = 0;
-        if (a.reward) a.reward[b] = 0;
-        if (a.done) a.done[b] = 0;
-        if (a.trunc) a.trunc[b] = 0;
-        if (a.flags) a.flags[b] = fa < 0 ? FLAG_NO_LEGAL : 0u;
-        uint8_t tmp[CF::N];
-        planes_to_bytes<CF>(P, tmp);
+        const uint32_t m397 = mt_state397(seed);
+        ChainMT mt;
+        mt.init(seed, m397);
+        if (!init_emit<CF>(a, b, seed, m397, mt)) {
+            const uint32_t slot = atomicAdd(a.ovf_count, 1u);
+            a.ovf_list[slot] = (uint32_t)b;
+        }
+    }
+}
+
+// ---- wave-cooperative reset for boards whose reset needs >= 624 draws ----
+// One board per wave. The 624-word MT19937 state sits in LDS; the twist runs
+// on all 64 lanes (three dependency phases), and randint(1, T+1) over the
+// board is a parallel filter: 64 raw outputs per trip, ballot of the accepted
+// ones, prefix popcount for their cell. The bitboard logic (get_matches
+// mask, legal, first action) runs redundantly on every lane, so control flow
+// stays wave-uniform. Latency ~tens of us instead of ~1 ms for one lane
+// walking the state.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void wave_twist(uint32_t* key, int lane) {  // numpy mt19937_gen
+    for (int base = 0; base < 227; base += 64) {  // mt'[i] = mt[i+397] ^ twist(mt[i], mt[i+1])
+        const int i = base + lane;
+        uint32_t a0 = 0, a1 = 0, x = 0;
+        if (i < 227) { a0 = key[i]; a1 = key[i + 1]; x = key[i + 397]; }
+        asm volatile("" ::: "memory");  // every lane's loads before any lane's store
+        if (i < 227) key[i] = x ^ mt_twist(a0, a1);
+        wave_sync();
+    }
+    for (int base = 227; base < 623; base += 64) {  // mt'[i] = mt'[i-227] ^ twist(mt[i], mt[i+1])
+        const int i = base + lane;
+        uint32_t a0 = 0, a1 = 0, x = 0;
+        if (i < 623) { a0 = key[i]; a1 = key[i + 1]; x = key[i - 227]; }
+        asm volatile("" ::: "memory");
+        if (i < 623) key[i] = x ^ mt_twist(a0, a1);
+        wave_sync();
+    }
+    if (lane == 0) key[623] = key[396] ^ mt_twist(key[623], key[0]);
+    wave_sync();
+}
+
+__device__ __forceinline__ int select_bit64(uint64_t m, int k) {
+    const uint32_t lo = (uint32_t)m;
+    const int c = __builtin_popcount(lo);
+    return k < c ? select_bit(lo, k) : 32 + select_bit((uint32_t)(m >> 32), k - c);
+}
+
+// RandomState.randint(1, T+1, (R, C)) into cells (only where `only` is set,
+// if given); advances (pos, k) over the LDS state exactly as numpy would.
+template <class CF>
+__device__ __forceinline__ void wave_fill(uint32_t* key, uint8_t* cells, int lane, uint32_t& pos, uint32_t& k,
+                                          const typename CF::Bd* only) {
+    int filled = 0;
+    while (filled < CF::N) {
+        if constexpr (CF::TILE_RNG == 0u) {  // randint(1, 2): no draws consumed
+            for (int c = lane; c < CF::N; c += 64)
+                if (!only || only->test(c)) cells[c] = 1;
+            break;
+        }
+        if (pos == 624u) {
+            wave_twist(key, lane);
+            pos = 0u;
+        }
+        const int take = (int)min(64u, 624u - pos);
+        uint32_t v = 0;
+        bool acc = false;
+        if (lane < take) {
+            v = mt_temper(key[pos + lane]) & CF::TILE_MASK;
+            acc = v <= CF::TILE_RNG;
+        }
+        const uint64_t bal = __ballot(acc);
+        const int rank = __builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        const int need = CF::N - filled, got = __builtin_popcountll(bal);
+        if (acc && rank < need) {
+            const int c = filled + rank;
+            if (!only || only->test(c)) cells[c] = (uint8_t)(v + 1u);
+        }
+        const int used = got >= need ? select_bit64(bal, need - 1) + 1 : take;
+        pos += (uint32_t)used;
+        k += (uint32_t)used;
+        filled += got >= need ? need : got;
+    }
+    wave_sync();
+}
+
+constexpr int WC_WAVES = 4;
+
+template <class CF>
+__global__ void __launch_bounds__(64 * WC_WAVES) k_init_fix(InitArgs a) {
+    __shared__ uint32_t key_s[WC_WAVES][624];
+    __shared__ __attribute__((aligned(16))) uint8_t cell_s[WC_WAVES][(CF::N + 3) / 4 * 4 + 16];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* key = key_s[wv];
+    uint8_t* cells = cell_s[wv];
+    const uint32_t cnt = *a.ovf_count;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(a.ovf_count + 7, cnt);  // stats: reset recomputes
+    for (uint32_t i = blockIdx.x * WC_WAVES + wv; i < cnt; i += gridDim.x * WC_WAVES) {
+        const int64_t b = a.ovf_list[i];
+        const uint32_t seed = a.seeds_out ? a.seeds_out[b] : a.seeds[b] + a.stride;
+        if (lane == 0) {  // init_genrand is a serial recurrence
+            uint32_t x = seed;
+            for (uint32_t p = 0; p < 624u; ++p) {
+                key[p] = x;
+                x = mt_init_next(x, p + 1u);
+            }
+        }
+        wave_sync();
+        const uint32_t m397 = key[397];
+        uint32_t pos = 624u, k = 0u;
+        wave_fill<CF>(key, cells, lane, pos, k, nullptr);                  // boardv2.py:21
+        typename CF::Bd P[CF::NP], mask;
+        planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
+        while (get_match_mask<CF>(P, mask)) {                               // boardv2.py:23-27
+            wave_fill<CF>(key, cells, lane, pos, k, &mask);
+            planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
+        }
+        if (lane == 0) init_outputs<CF>(a, b, seed, m397, k, P);
         int8_t* dst = a.boards + b * CF::N;
-        for (int x = 0; x < CF::N; ++x) dst[x] = (int8_t)tmp[x];
+        for (int x = lane; x < CF::N; x += 64) dst[x] = (int8_t)cells[x];
+        wave_sync();
     }
 }
 
 template <class CF>
-__global__ void __launch_bounds__(BLOCK) k_legal(int64_t n, const int8_t* boards, uint32_t* legal) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BLOCK * CF::N + 16];
-    const int64_t b0 = (int64_t)blockIdx.x * BLOCK;
-    const int nb = (int)((n - b0) < BLOCK ? (n - b0) : BLOCK);
-    block_copy_in<CF::N>(boards + b0 * CF::N, lds, nb);
+__global__ void __launch_bounds__(KS<CF>::B) k_legal(int64_t n, const int8_t* boards, uint32_t* legal) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[KS<CF>::B * CF::N + 16];
+    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
+    const int nb = (int)((n - b0) < KS<CF>::B ? (n - b0) : KS<CF>::B);
+    block_copy_in<CF::N, KS<CF>::B>(boards + b0 * CF::N, lds, nb);
     __syncthreads();
     const int t = threadIdx.x;
     if (t < nb) {
@@ -331,14 +518,14 @@ struct EnvArgs {
 };
 
 // Match3Env.step bookkeeping (env.py:48-56) around BoardV2.apply_action.
-template <class CF, class RNG>
-__device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng) {
+template <class CF, class RNG, class Store>
+__device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st) {
     const int act_in = a.actions ? a.actions[b] : a.next_action[b];
     const int mv = a.moves[b];
     typename CF::Bd HL, VL;
     uint32_t f;
-    const int r = apply_action<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL);
-    if (f & FLAG_RNG_OVERFLOW) return false;
+    const int r = apply_action<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st);
+    if (f & FLAG_RECOMPUTE) return false;
     const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
     const int sc = a.score[b] + r;
     const int mv1 = mv + 1;
@@ -369,11 +556,12 @@ __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& 
 }
 
 template <class CF>
-__global__ void __launch_bounds__(BLOCK) k_env_step(EnvArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BLOCK * CF::N + 16];
-    const int64_t b0 = (int64_t)blockIdx.x * BLOCK;
-    const int nb = (int)((a.n - b0) < BLOCK ? (a.n - b0) : BLOCK);
-    block_copy_in<CF::N>(a.cur + b0 * CF::N, lds, nb);
+__global__ void __launch_bounds__(KS<CF>::B) k_env_step(EnvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[KS<CF>::B * CF::N + 16];
+    __shared__ uint32_t gtab[LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::WORDS];
+    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
+    const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
+    block_copy_in<CF::N, KS<CF>::B>(a.cur + b0 * CF::N, lds, nb);
     __syncthreads();
     const int t = threadIdx.x;
     if (t < nb) {
@@ -382,26 +570,29 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvArgs a) {
         lds_to_planes<CF>(lds, t, P);
         ChainMT rng;
         rng.init(a.seeds[b], a.mt397[b]);
-        if (!env_step_one<CF>(P, a, b, rng)) {
+        LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};
+        if (!env_step_one<CF>(P, a, b, rng, st)) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
             a.ovf_list[slot] = (uint32_t)b;
         }
         planes_to_bytes<CF>(P, lds + t * CF::N);
     }
     __syncthreads();
-    block_copy_out<CF::N>(a.nxt + b0 * CF::N, lds, nb);
+    block_copy_out<CF::N, KS<CF>::B>(a.nxt + b0 * CF::N, lds, nb);
 }
 
 template <class CF>
 __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
     const uint32_t cnt = a.counters[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.counters[8], cnt);  // stats: step recomputes
     for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.cur + b * CF::N, P);
-        FullMT mt;
+        FullMT mt;  // scratch (see k_apply_fix)
         mt.init(a.seeds[b], 0u);
-        env_step_one<CF>(P, a, b, mt);
+        ArrayStore<CF> st;
+        env_step_one<CF>(P, a, b, mt, st);
         uint8_t tmp[CF::N];
         planes_to_bytes<CF>(P, tmp);
         for (int x = 0; x < CF::N; ++x) a.nxt[b * CF::N + x] = (int8_t)tmp[x];
@@ -455,7 +646,7 @@ struct m3_env {
     uint8_t *done = nullptr, *trunc = nullptr;
     int32_t* actions = nullptr;
     uint32_t* counters = nullptr;
-    uint32_t *ovf_list = nullptr, *reset_list = nullptr;
+    uint32_t *ovf_list = nullptr, *reset_list = nullptr, *init_ovf_list = nullptr;
     int32_t* packed = nullptr;
     int32_t* gathered = nullptr;
     ncclComm_t comm = nullptr;
@@ -464,6 +655,17 @@ struct m3_env {
     // the i-th k_env_step launch since m3_env_timing(enable)
     std::vector<hipEvent_t> tev;
     int tcap = 0, tn = 0;
+    // Independent board shards, one HIP stream each. A shard's step ->
+    // fixup -> reset chain is serial, but the reset of a finished shard is a
+    // small latency-bound launch that overlaps the other shards' step kernels.
+    struct Shard {
+        int64_t off = 0, n = 0;
+        hipStream_t stream = nullptr;
+        hipEvent_t ev = nullptr;
+    };
+    std::vector<Shard> shards;
+    hipEvent_t gather_ev = nullptr;
+    bool gather_pending = false;
 };
 
 namespace {
@@ -496,25 +698,29 @@ size_t carve_size(std::initializer_list<size_t> sizes) {
     return s + 256;
 }
 
-int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
+template <class CF>
+int grid_for(int64_t n) { return (int)((n + KS<CF>::B - 1) / KS<CF>::B); }
 
 template <class CF>
 int launch_apply(m3_ctx* c, const ApplyArgs& a) {
     if (a.n == 0) return M3_OK;
     HIP_TRY(hipMemsetAsync(a.ovf_count, 0, sizeof(uint32_t), c->stream));
-    hipLaunchKernelGGL(k_apply<CF>, dim3(grid_for(a.n)), dim3(BLOCK), 0, c->stream, a);
+    hipLaunchKernelGGL(k_apply<CF>, dim3(grid_for<CF>(a.n)), dim3(KS<CF>::B), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_apply_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }
 
+// ovf_count must be zeroed on the stream before this call.
 template <class CF>
-int launch_init(m3_ctx* c, const InitArgs& a, int64_t max_items) {
+int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     if (max_items == 0) return M3_OK;
-    int64_t g = grid_for(max_items);
+    int64_t g = (max_items + INIT_BLOCK - 1) / INIT_BLOCK;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(BLOCK), 0, c->stream, a);
+    hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_init_fix<CF>, dim3(FIX_GRID), dim3(64 * WC_WAVES), 0, stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }
@@ -522,67 +728,105 @@ int launch_init(m3_ctx* c, const InitArgs& a, int64_t max_items) {
 template <class CF>
 int launch_legal(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* legal) {
     if (n == 0) return M3_OK;
-    hipLaunchKernelGGL(k_legal<CF>, dim3(grid_for(n)), dim3(BLOCK), 0, c->stream, n, boards, legal);
+    hipLaunchKernelGGL(k_legal<CF>, dim3(grid_for<CF>(n)), dim3(KS<CF>::B), 0, c->stream, n, boards, legal);
     HIP_TRY(hipGetLastError());
+    return M3_OK;
+}
+
+// Enqueue one env step of shard s on its stream: zero the shard's counters,
+// k_env_step (cur -> nxt), k_env_fix (recompute overflowed boards), and with
+// autoreset k_init + k_init_fix over the boards that finished. Every pointer
+// is offset to the shard, so kernels see shard-local board indices.
+template <class CF>
+int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
+    m3_ctx* c = e->ctx;
+    const m3_env::Shard& sh = e->shards[s];
+    if (sh.n == 0) return M3_OK;
+    const int64_t o = sh.off;
+    const int N = c->N, AW = c->AW;
+    uint32_t* cnt = e->counters + 64 * s;
+    hipStream_t st = sh.stream;
+    if (e->gather_pending) HIP_TRY(hipStreamWaitEvent(st, e->gather_ev, 0));  // `packed` still being read
+    EnvArgs a;
+    a.n = sh.n;
+    a.num_moves = e->num_moves;
+    a.goal = e->goal;
+    a.autoreset = e->autoreset;
+    a.cur = e->boards[e->cur] + o * N;
+    a.nxt = e->boards[e->cur ^ 1] + o * N;
+    a.actions = d_actions ? d_actions + o : nullptr;
+    a.seeds = e->seeds + o;
+    a.mt397 = e->mt397 + o;
+    a.score = e->score + o;
+    a.moves = e->moves + o;
+    a.next_action = e->next_action + o;
+    a.reward = e->reward + o;
+    a.done = e->done + o;
+    a.trunc = e->trunc + o;
+    a.flags = e->flags + o;
+    a.draws = e->draws + o;
+    a.legal = e->legal + o * AW;
+    a.packed = e->packed + o;
+    a.counters = cnt;
+    a.ovf_list = e->ovf_list + o;
+    a.reset_list = e->reset_list + o;
+    HIP_TRY(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
+    const bool timed = e->tn < e->tcap;
+    if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], st));
+    hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    if (timed) {
+        HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], st));
+        e->tn++;
+    }
+    hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    if (e->autoreset) {
+        InitArgs r{};
+        r.n = sh.n;
+        r.seeds = e->seeds + o;
+        r.list = e->reset_list + o;
+        r.list_count = &cnt[1];
+        r.stride = e->stride;
+        r.seeds_out = e->seeds + o;
+        r.boards = e->boards[e->cur ^ 1] + o * N;
+        r.first_action = e->next_action + o;
+        r.legal = e->legal + o * AW;
+        r.mt397 = e->mt397 + o;
+        r.score = e->score + o;
+        r.moves = e->moves + o;
+        r.ovf_count = &cnt[2];
+        r.ovf_list = e->init_ovf_list + o;
+        // reward/done/trunc/flags of the finished step stay visible; the grid
+        // is sized for the expected number of finished boards and grid-strides
+        int rc = launch_init<CF>(st, r, sh.n / 8 + 1);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipEventRecord(sh.ev, st));
     return M3_OK;
 }
 
 template <class CF>
 int launch_env_step(m3_env* e, const int32_t* d_actions) {
-    m3_ctx* c = e->ctx;
-    EnvArgs a;
-    a.n = e->n;
-    a.num_moves = e->num_moves;
-    a.goal = e->goal;
-    a.autoreset = e->autoreset;
-    a.cur = e->boards[e->cur];
-    a.nxt = e->boards[e->cur ^ 1];
-    a.actions = d_actions;
-    a.seeds = e->seeds;
-    a.mt397 = e->mt397;
-    a.score = e->score;
-    a.moves = e->moves;
-    a.next_action = e->next_action;
-    a.reward = e->reward;
-    a.done = e->done;
-    a.trunc = e->trunc;
-    a.flags = e->flags;
-    a.draws = e->draws;
-    a.legal = e->legal;
-    a.packed = e->packed;
-    a.counters = e->counters;
-    a.ovf_list = e->ovf_list;
-    a.reset_list = e->reset_list;
-    HIP_TRY(hipMemsetAsync(e->counters, 0, 2 * sizeof(uint32_t), c->stream));
-    const bool timed = e->tn < e->tcap;
-    if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], c->stream));
-    hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for(e->n)), dim3(BLOCK), 0, c->stream, a);
-    HIP_TRY(hipGetLastError());
-    if (timed) {
-        HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], c->stream));
-        e->tn++;
-    }
-    hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
-    HIP_TRY(hipGetLastError());
-    e->cur ^= 1;
-    if (e->autoreset) {
-        InitArgs r{};
-        r.n = e->n;
-        r.seeds = e->seeds;
-        r.list = e->reset_list;
-        r.list_count = &e->counters[1];
-        r.stride = e->stride;
-        r.seeds_out = e->seeds;
-        r.boards = e->boards[e->cur];
-        r.first_action = e->next_action;
-        r.legal = e->legal;
-        r.mt397 = e->mt397;
-        r.score = e->score;
-        r.moves = e->moves;
-        // reward/done/trunc/flags of the finished step stay visible
-        int rc = launch_init<CF>(c, r, e->n);
+    for (int s = 0; s < (int)e->shards.size(); ++s) {
+        int rc = launch_env_shard<CF>(e, s, d_actions);
         if (rc) return rc;
     }
+    e->gather_pending = false;
+    e->cur ^= 1;
+    return M3_OK;
+}
+
+// Make `st` wait for every shard's last enqueued work.
+int join_shards(m3_env* e, hipStream_t st) {
+    for (auto& sh : e->shards)
+        if (sh.n) HIP_TRY(hipStreamWaitEvent(st, sh.ev, 0));
+    return M3_OK;
+}
+
+int sync_env(m3_env* e) {
+    for (auto& sh : e->shards) HIP_TRY(hipStreamSynchronize(sh.stream));
+    HIP_TRY(hipStreamSynchronize(e->ctx->stream));
     return M3_OK;
 }
 
@@ -685,7 +929,7 @@ int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boar
     CHECK_ARG(c && n >= 0 && (n == 0 || (seeds && out_boards)), "bad arguments");
     if (n == 0) return M3_OK;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t need = carve_size({n * 4ull, n * (size_t)c->N, n * 4ull, n * 4ull});
+    const size_t need = carve_size({n * 4ull, n * (size_t)c->N, n * 4ull, n * 4ull, n * 4ull});
     int rc = ensure_scratch(c, need);
     if (rc) return rc;
     Carve cv{(char*)c->dbuf};
@@ -694,13 +938,16 @@ int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boar
     uint32_t* d_draws = cv.take<uint32_t>(n);
     int32_t* d_first = cv.take<int32_t>(n);
     HIP_TRY(hipMemcpyAsync(d_seeds, seeds, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, 16, c->stream));
     InitArgs a{};
     a.n = n;
     a.seeds = d_seeds;
     a.boards = d_boards;
     a.draws = d_draws;
     a.first_action = d_first;
-    rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c, a, n); });
+    a.ovf_count = &c->counters[1];
+    a.ovf_list = cv.take<uint32_t>(n);
+    rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, n); });
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(out_boards, d_boards, n * c->N, hipMemcpyDeviceToHost, c->stream));
     if (out_draws) HIP_TRY(hipMemcpyAsync(out_draws, d_draws, n * 4, hipMemcpyDeviceToHost, c->stream));
@@ -810,25 +1057,67 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     alloc(&e->done, n);
     alloc(&e->trunc, n);
     alloc(&e->actions, n * 4);
-    alloc(&e->counters, 256);
+    alloc(&e->counters, 64 * 4 * MAX_SHARDS);
     alloc(&e->ovf_list, n * 4);
     alloc(&e->reset_list, n * 4);
+    alloc(&e->init_ovf_list, n * 4);
     alloc(&e->packed, n * 4);
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&e->gather_ev, hipEventDisableTiming);
     if (err != hipSuccess) {
         m3_env_destroy(e);
         return set_err(M3_ERR_HIP, "env allocation (%lld boards): %s", (long long)n, hipGetErrorString(err));
+    }
+    // default sharding: one shard per 256k boards, at most 4
+    int rc = m3_env_set_shards(e, (int)std::min<int64_t>(4, std::max<int64_t>(1, n / (1 << 18))));
+    if (rc) {
+        m3_env_destroy(e);
+        return rc;
     }
     *out = e;
     return M3_OK;
 }
 
+int m3_env_set_shards(m3_env* e, int nshards) {
+    CHECK_ARG(e && nshards >= 1 && nshards <= MAX_SHARDS, "nshards must be in [1, 8]");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    int rc = sync_env(e);
+    if (rc) return rc;
+    for (auto& sh : e->shards) {
+        (void)hipStreamDestroy(sh.stream);
+        (void)hipEventDestroy(sh.ev);
+    }
+    e->shards.clear();
+    // shard boundaries on 256-board workgroup multiples
+    const int64_t per = ((e->n + nshards - 1) / nshards + BLOCK - 1) / BLOCK * BLOCK;
+    for (int s = 0; s < nshards; ++s) {
+        m3_env::Shard sh;
+        sh.off = std::min<int64_t>(e->n, s * per);
+        sh.n = std::min<int64_t>(e->n, sh.off + per) - sh.off;
+        HIP_TRY(hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&sh.ev, hipEventDisableTiming));
+        e->shards.push_back(sh);
+    }
+    return M3_OK;
+}
+
+int m3_env_synchronize(m3_env* e) {
+    CHECK_ARG(e, "null env");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    return sync_env(e);
+}
+
 int m3_env_destroy(m3_env* e) {
     if (!e) return M3_OK;
     (void)hipSetDevice(e->ctx->device);
-    (void)hipStreamSynchronize(e->ctx->stream);
+    (void)sync_env(e);
+    for (auto& sh : e->shards) {
+        (void)hipStreamDestroy(sh.stream);
+        (void)hipEventDestroy(sh.ev);
+    }
+    if (e->gather_ev) (void)hipEventDestroy(e->gather_ev);
     void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->mt397, e->flags, e->draws, e->legal,
                     e->score, e->moves, e->next_action, e->reward, e->done, e->trunc, e->actions,
-                    e->counters, e->ovf_list, e->reset_list, e->packed, e->gathered};
+                    e->counters, e->ovf_list, e->reset_list, e->init_ovf_list, e->packed, e->gathered};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (e->comm) ncclCommDestroy(e->comm);
@@ -841,6 +1130,8 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     CHECK_ARG(e, "null env");
     m3_ctx* c = e->ctx;
     HIP_TRY(hipSetDevice(c->device));
+    int rc0 = sync_env(e);
+    if (rc0) return rc0;
     if (seeds) {
         HIP_TRY(hipMemcpyAsync(e->seeds, seeds, e->n * 4, hipMemcpyHostToDevice, c->stream));
     } else {
@@ -866,7 +1157,10 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     a.trunc = e->trunc;
     a.flags = e->flags;
     a.draws = e->draws;
-    int rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c, a, e->n); });
+    a.ovf_count = &e->counters[2];
+    a.ovf_list = e->init_ovf_list;
+    HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));  // also clears the stats
+    int rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, e->n); });
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     e->ready = true;
@@ -890,8 +1184,16 @@ int m3_env_step_device(m3_env* e, const int32_t* d_actions) {
 int m3_env_step(m3_env* e, const int32_t* actions) {
     CHECK_ARG(e, "null env");
     if (actions) {
+        // the previous step may still read e->actions: order the upload after
+        // every shard, and every shard of this step after the upload
         HIP_TRY(hipSetDevice(e->ctx->device));
-        HIP_TRY(hipMemcpyAsync(e->actions, actions, e->n * 4, hipMemcpyHostToDevice, e->ctx->stream));
+        hipStream_t st = e->ctx->stream;
+        int rc = join_shards(e, st);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(e->actions, actions, e->n * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(e->gather_ev, st));
+        e->gather_pending = true;
+        HIP_TRY(hipStreamSynchronize(st));  // `actions` is a caller-owned host buffer
         return m3_env_step_device(e, e->actions);
     }
     return m3_env_step_device(e, nullptr);
@@ -922,6 +1224,8 @@ int m3_env_get(m3_env* e, int what, void* host_out) {
     int rc = env_field(e, what, &p, &bytes);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(e->ctx->device));
+    rc = join_shards(e, e->ctx->stream);
+    if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(host_out, p, bytes, hipMemcpyDeviceToHost, e->ctx->stream));
     HIP_TRY(hipStreamSynchronize(e->ctx->stream));
     return M3_OK;
@@ -958,7 +1262,11 @@ int m3_env_gather(m3_env* e, int32_t* host_out) {
     CHECK_ARG(e, "null env");
     if (!e->comm) return set_err(M3_ERR_STATE, "m3_env_gather before m3_env_comm_init");
     HIP_TRY(hipSetDevice(e->ctx->device));
+    int rc = join_shards(e, e->ctx->stream);  // every shard's packed words written
+    if (rc) return rc;
     RCCL_TRY(ncclAllGather(e->packed, e->gathered, (size_t)e->n, ncclInt32, e->comm, e->ctx->stream));
+    HIP_TRY(hipEventRecord(e->gather_ev, e->ctx->stream));  // next step must not overwrite `packed` early
+    e->gather_pending = true;
     if (host_out) {
         HIP_TRY(hipMemcpyAsync(host_out, e->gathered, (size_t)e->nranks * e->n * 4, hipMemcpyDeviceToHost,
                                e->ctx->stream));
@@ -967,10 +1275,28 @@ int m3_env_gather(m3_env* e, int32_t* host_out) {
     return M3_OK;
 }
 
+int m3_env_stats(m3_env* e, uint64_t out[4]) {
+    CHECK_ARG(e && out, "bad arguments");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    int rc = sync_env(e);
+    if (rc) return rc;
+    std::vector<uint32_t> h(64 * MAX_SHARDS);
+    HIP_TRY(hipMemcpy(h.data(), e->counters, h.size() * 4, hipMemcpyDeviceToHost));
+    out[0] = out[1] = out[2] = out[3] = 0;
+    for (size_t s = 0; s < e->shards.size(); ++s) {
+        out[0] += h[64 * s + 8];   // steps recomputed (>= 624 draws or > table groups)
+        out[1] += h[64 * s + 9];   // resets recomputed by the wave-cooperative pass (>= 624 draws)
+        out[2] += h[64 * s + 10];  // autoresets
+    }
+    out[3] = e->shards.size();
+    return M3_OK;
+}
+
 int m3_env_timing(m3_env* e, int capacity) {
     CHECK_ARG(e && capacity >= 0, "bad arguments");
     HIP_TRY(hipSetDevice(e->ctx->device));
-    HIP_TRY(hipStreamSynchronize(e->ctx->stream));
+    int rc = sync_env(e);
+    if (rc) return rc;
     while ((int)e->tev.size() < 2 * capacity) {
         hipEvent_t ev;
         HIP_TRY(hipEventCreate(&ev));
@@ -985,7 +1311,8 @@ int m3_env_kernel_ms(m3_env* e, float* out_ms, int max_n, int* out_n) {
     CHECK_ARG(e && out_n && (max_n == 0 || out_ms), "bad arguments");
     HIP_TRY(hipSetDevice(e->ctx->device));
     const int n = e->tn < max_n ? e->tn : max_n;
-    if (n > 0) HIP_TRY(hipEventSynchronize(e->tev[2 * (n - 1) + 1]));
+    int rc = sync_env(e);
+    if (rc) return rc;
     for (int i = 0; i < n; ++i) HIP_TRY(hipEventElapsedTime(&out_ms[i], e->tev[2 * i], e->tev[2 * i + 1]));
     *out_n = n;
     return M3_OK;

@@ -61,9 +61,12 @@ struct BB {
         _Pragma("unroll") for (int i = 0; i < W; ++i) r.w[i] = (q == i) ? b : 0u;
         return r;
     }
+    // Dynamic word select written as masks, not a select chain: LLVM turns a
+    // select chain over several boards into a stack array + indexed scratch
+    // load, which costs a memory round trip on the GPU.
     M3_HD uint32_t word_at(int q) const {
-        uint32_t v = w[0];
-        _Pragma("unroll") for (int i = 1; i < W; ++i) v = (q == i) ? w[i] : v;
+        uint32_t v = 0u;
+        _Pragma("unroll") for (int i = 0; i < W; ++i) v |= w[i] & (0u - (uint32_t)(q == i));
         return v;
     }
     M3_HD uint32_t test(int x) const { return (word_at(x >> 5) >> (x & 31)) & 1u; }

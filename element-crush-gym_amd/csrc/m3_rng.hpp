@@ -49,7 +49,13 @@ M3_HD uint32_t mt_state397(uint32_t seed) {
     return x;
 }
 
-struct ChainMT {
+// LIMIT = 624: three chain levels, every draw of the first MT block.
+// LIMIT = 227: one level; draw 227 raises `overflow` (the step kernels use
+// this: a step needs > 226 draws essentially never, and one level keeps five
+// fewer VGPRs live through the cascade).
+template <uint32_t LIMIT>
+struct ChainMTT {
+    static_assert(LIMIT == 227u || LIMIT == 624u, "chain depth");
     uint32_t seed, mt397;
     uint32_t k;           // raw outputs since the last reseed
     uint32_t a_lo, a_hi;  // mt[k], mt[k+397]
@@ -85,7 +91,7 @@ struct ChainMT {
 
   private:
     M3_HD uint32_t slow(uint32_t i) {
-        if (i >= 624u) {
+        if (i >= LIMIT) {
             overflow = 1u;
             return 0u;
         }
@@ -126,6 +132,8 @@ struct ChainMT {
         return vb ^ twa;
     }
 };
+using ChainMT = ChainMTT<624u>;
+using ChainMT1 = ChainMTT<227u>;
 
 // Textbook MT19937 (numpy mt19937_seed / mt19937_gen / mt19937_next32).
 struct FullMT {

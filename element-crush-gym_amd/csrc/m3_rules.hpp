@@ -36,6 +36,8 @@ enum : uint32_t {
     FLAG_NO_LEGAL = 0x08u,     // no legal action to sample (np.random.choice([]) raises)
     FLAG_SHUFFLED = 0x10u,     // the dead-board shuffle ran at least once
     FLAG_RNG_OVERFLOW = 0x20u, // internal: step needed >= 624 draws; recomputed with FullMT
+    FLAG_GROUP_OVERFLOW = 0x40u, // internal: more match groups than the fast table holds; recomputed
+    FLAG_RECOMPUTE = FLAG_RNG_OVERFLOW | FLAG_GROUP_OVERFLOW,
 };
 
 // BoardConfig (match3tile/boardConfig.py:26-43) as compile-time constants.
@@ -56,6 +58,9 @@ struct Cfg {
     static constexpr int NP = 7;                 // value planes for int8 cells in [0, 127]
     static constexpr int MAXG = N / 3 + 1;       // run-disjoint group creators, >= 3 cells each
     static constexpr int SHUFFLE_CAP = 1024;
+    // randint(1, T+1) = 1 + masked-rejection draw on [0, T-1]
+    static constexpr uint32_t TILE_RNG = (uint32_t)(T - 1);
+    static constexpr uint32_t TILE_MASK = (1u << ceil_log2(T)) - 1u;
     static_assert(R >= 4 && C >= 4 && R <= 16 && C <= 16, "board size");
     static_assert(T >= 1 && BITS <= 4, "tile types must fit 4 bits");
     using Bd = BB<W>;
@@ -96,10 +101,10 @@ M3_HD typename CF::Bd tb_eq(const typename CF::Bd* P) {
 
 template <class CF, int NPU>
 M3_HD int cell_value(const typename CF::Bd* P, int x) {
-    const int q = x >> 5, s = x & 31;
+    const typename CF::Bd bm = CF::Bd::bit_at(x);
     int v = 0;
 #pragma unroll
-    for (int p = 0; p < NPU; ++p) v |= (int)((P[p].word_at(q) >> s) & 1u) << p;
+    for (int p = 0; p < NPU; ++p) v |= (int)((P[p] & bm).any()) << p;
     return v;
 }
 
@@ -259,11 +264,38 @@ M3_HD int random_action(const uint32_t* act, RNG& rng) {
 // the three value planes BITS..BITS+2 (H = bit BITS, V = bit BITS+1, B = both,
 // M = bit BITS+2).
 // --------------------------------------------------------------------------
+// Group tables. get_matches only touches a group through get_h/get_v/put, so
+// the storage is pluggable: the HIP kernels keep a small per-lane table in LDS
+// (m3_api.hip, LdsStore) and report overflow; the fallback pass and the host
+// harness use ArrayStore, which can hold every group a board can form.
 template <class CF>
-struct Groups {
-    typename CF::Bd h[CF::MAXG];
-    typename CF::Bd v[CF::MAXG];
+struct ArrayStore {
+    static constexpr int CAP = CF::MAXG;
+    typename CF::Bd h[CAP];
+    typename CF::Bd v[CAP];
+    M3_HD typename CF::Bd get_h(int g) const { return h[g]; }
+    M3_HD typename CF::Bd get_v(int g) const { return v[g]; }
+    M3_HD void put(int g, const typename CF::Bd& hh, const typename CF::Bd& vv) {
+        h[g] = hh;
+        v[g] = vv;
+    }
 };
+
+// A deliberately tiny table (test harness): forces the overflow path.
+template <class CF, int CAP_>
+struct SmallStore {
+    static constexpr int CAP = CAP_;
+    typename CF::Bd h[CAP];
+    typename CF::Bd v[CAP];
+    M3_HD typename CF::Bd get_h(int g) const { return h[g]; }
+    M3_HD typename CF::Bd get_v(int g) const { return v[g]; }
+    M3_HD void put(int g, const typename CF::Bd& hh, const typename CF::Bd& vv) {
+        h[g] = hh;
+        v[g] = vv;
+    }
+};
+
+enum : int { MATCH_NONE = 0, MATCH_FOUND = 1, MATCH_OVERFLOW = -1 };
 
 template <class CF>
 M3_HD int multiset_select(const typename CF::Bd& hg, const typename CF::Bd& vg, int k) {
@@ -285,8 +317,14 @@ M3_HD int multiset_select(const typename CF::Bd& hg, const typename CF::Bd& vg, 
     return 0;
 }
 
-template <class CF, bool SPAWN>
-M3_HD bool get_matches(const typename CF::Bd* P, typename CF::Bd& mask, typename CF::Bd* sw) {
+struct NoStore {
+    static constexpr int CAP = 0;
+};
+
+// Returns MATCH_NONE / MATCH_FOUND, or MATCH_OVERFLOW when SPAWN needs more
+// groups than Store::CAP (the caller then recomputes with ArrayStore).
+template <class CF, bool SPAWN, class Store>
+M3_HD int match_scan(const typename CF::Bd* P, typename CF::Bd& mask, typename CF::Bd* sw, Store& st) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
     constexpr int C = CF::C, R = CF::R;
@@ -304,13 +342,12 @@ M3_HD bool get_matches(const typename CF::Bd* P, typename CF::Bd& mask, typename
         sw[1] = Bd::zero();
         sw[2] = Bd::zero();
     }
-    if (!cand.any()) return false;
+    if (!cand.any()) return MATCH_NONE;
 
     // doubling link masks for run floods (runs are <= 16 long)
     const Bd dh2 = e1h & at<1>(e1h), dh4 = dh2 & at<2>(dh2), dh8 = dh4 & at<4>(dh4);
     const Bd dv2 = e1v & at<C>(e1v), dv4 = dv2 & at<2 * C>(dv2), dv8 = dv4 & at<4 * C>(dv4);
 
-    Groups<CF> grp;
     int ng = 0;
     Bd vruns = Bd::zero();
     while (cand.any()) {                                       // row-major scan over run starts
@@ -338,23 +375,21 @@ M3_HD bool get_matches(const typename CF::Bd* P, typename CF::Bd& mask, typename
             int g = -1;
             if ((rh & vruns).any()) {                          // add_to_matches (:126-131)
                 for (int gi = 0; gi < ng; ++gi) {
-                    if ((grp.v[gi] & rh).any()) { g = gi; break; }
+                    if ((st.get_v(gi) & rh).any()) { g = gi; break; }
                 }
             }
             if (g < 0) {
-                g = ng++;
-                grp.h[g] = rh;
-                grp.v[g] = rv;
+                if (ng == Store::CAP) return MATCH_OVERFLOW;
+                st.put(ng++, rh, rv);
             } else {
-                grp.h[g] |= rh;
-                grp.v[g] |= rv;
+                st.put(g, st.get_h(g) | rh, st.get_v(g) | rv);
             }
             vruns |= rv;
         }
     }
     if constexpr (SPAWN) {
         for (int gi = 0; gi < ng; ++gi) {                      // get_match_spawn_mask (:159-169)
-            const Bd hg = grp.h[gi], vg = grp.v[gi];
+            const Bd hg = st.get_h(gi), vg = st.get_v(gi);
             const int len = hg.popc() + vg.popc();
             if (len <= 3) continue;
             int centre, kind;  // kind bits: 1 = plane BITS, 2 = BITS+1, 4 = BITS+2
@@ -377,7 +412,19 @@ M3_HD bool get_matches(const typename CF::Bd* P, typename CF::Bd& mask, typename
             if (kind & 4) sw[2] |= bm;
         }
     }
-    return true;
+    return MATCH_FOUND;
+}
+
+template <class CF, class Store>
+M3_HD int get_matches(const typename CF::Bd* P, typename CF::Bd& mask, typename CF::Bd* sw, Store& st) {
+    return match_scan<CF, true>(P, mask, sw, st);
+}
+
+// mask only (BoardV2.__init__ only asks "any match?" and which cells)
+template <class CF>
+M3_HD bool get_match_mask(const typename CF::Bd* P, typename CF::Bd& mask) {
+    NoStore ns;
+    return match_scan<CF, false>(P, mask, nullptr, ns) != MATCH_NONE;
 }
 
 // --------------------------------------------------------------------------
@@ -503,9 +550,19 @@ M3_HD void gravity_refill(typename CF::Bd* P, RNG& rng) {
     uint32_t tops = em.w[0] & ((1u << C) - 1u);  // columns with at least one empty cell
     int c = __builtin_ctz(tops);
     int r = 0;
-    constexpr uint32_t RNGT = (uint32_t)(CF::T - 1);
+    // One raw draw per loop trip (the masked-rejection of randint(1, T+1) is
+    // folded into the trip count): with a nested rejection loop per tile the
+    // wave would wait for its unluckiest lane on every tile.
     for (;;) {
-        const uint32_t v = rand_masked(rng, RNGT) + 1u;   // randint(1, T+1)
+        uint32_t v;
+        if constexpr (CF::TILE_RNG == 0u) {
+            v = 1u;
+        } else {
+            v = rng.next32() & CF::TILE_MASK;
+            if (rng.overflow) break;
+            if (v > CF::TILE_RNG) continue;
+            v += 1u;                                       // randint(1, T+1)
+        }
         const int x = r * C + c;
         const Bd bm = Bd::bit_at(x);
 #pragma unroll
@@ -522,7 +579,6 @@ M3_HD void gravity_refill(typename CF::Bd* P, RNG& rng) {
             c = __builtin_ctz(tops);
             r = 0;
         }
-        if (rng.overflow) break;
     }
 }
 
@@ -571,9 +627,9 @@ M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng) {
 // P: NP planes in/out. Returns the step reward; sets flags/draws and the
 // legal masks of the resulting board.
 // --------------------------------------------------------------------------
-template <class CF, class RNG>
+template <class CF, class RNG, class Store>
 M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, uint32_t& flags,
-                       typename CF::Bd& HL, typename CF::Bd& VL) {
+                       typename CF::Bd& HL, typename CF::Bd& VL, Store& st) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
     constexpr int C = CF::C, R = CF::R, TM = CF::TM;
@@ -629,7 +685,10 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
     } else if (are(H, V)) {                                     // :130-132 rows < t.col, rows >= t.row
         zr = G::row_band(0, tc < R ? tc : R) | G::row_band(tr, R);
     } else {                                                    // :133-136
-        get_matches<CF, true>(P, zr, sw);
+        if (get_matches<CF>(P, zr, sw, st) == MATCH_OVERFLOW) {
+            flags |= FLAG_GROUP_OVERFLOW;
+            return 0;
+        }
     }
     int reward = 0;
     // first pass with all 7 planes (input values may exceed 32 until the clip)
@@ -641,7 +700,12 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
         gravity_refill<CF>(P, rng);                             // :166-173
         if (rng.overflow) break;
         Bd mask;
-        bool found = get_matches<CF, true>(P, mask, sw);        // :176-181
+        int mr = get_matches<CF>(P, mask, sw, st);              // :176-181
+        if (mr == MATCH_OVERFLOW) {
+            flags |= FLAG_GROUP_OVERFLOW;
+            return 0;
+        }
+        bool found = mr == MATCH_FOUND;
         if (!found) {
             legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
             int shuffles = 0;
@@ -653,7 +717,12 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
                 shuffle_rows<CF>(P, rng);
                 flags |= FLAG_SHUFFLED;
                 ++shuffles;
-                found = get_matches<CF, true>(P, mask, sw);
+                mr = get_matches<CF>(P, mask, sw, st);
+                if (mr == MATCH_OVERFLOW) {
+                    flags |= FLAG_GROUP_OVERFLOW;
+                    return 0;
+                }
+                found = mr == MATCH_FOUND;
                 if (!found) legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
             }
             if (!found) break;                                   // :195-196
@@ -674,27 +743,28 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
 template <class CF, class RNG>
 M3_HD void init_board(typename CF::Bd* P, RNG& mt) {
     using Bd = typename CF::Bd;
-    constexpr uint32_t RNGT = (uint32_t)(CF::T - 1);
 #pragma unroll
     for (int p = 0; p < CF::NP; ++p) P[p] = Bd::zero();
-    for (int x = 0; x < CF::N; ++x) {                          // :21 randint(1, T+1, (R, C))
-        const uint32_t v = rand_masked(mt, RNGT) + 1u;
-        const Bd bm = Bd::bit_at(x);
-#pragma unroll
-        for (int p = 0; p < CF::BITS; ++p) {
-            const uint32_t on = 0u - ((v >> p) & 1u);
-#pragma unroll
-            for (int i = 0; i < CF::W; ++i) P[p].w[i] |= bm.w[i] & on;
+    // randint(1, T+1, (R, C)) fills cells in row-major order; as in the
+    // refill, one raw draw per loop trip so lanes never wait on each other's
+    // rejections. `take` = the value was accepted and belongs to cell x.
+    auto fill = [&](const Bd* only) {
+        int x = 0;
+        while (x < CF::N) {
+            uint32_t v = 1u;
+            if constexpr (CF::TILE_RNG != 0u) {
+                v = mt.next32() & CF::TILE_MASK;
+                if (mt.overflow) return;
+                if (v > CF::TILE_RNG) continue;
+                v += 1u;
+            }
+            if (!only || only->test(x)) set_cell<CF, CF::BITS>(P, x, (int)v);
+            ++x;
         }
-    }
+    };
+    fill(nullptr);                                             // :21
     Bd mask;
-    Bd* none = nullptr;
-    while (get_matches<CF, false>(P, mask, none)) {            // :23-27
-        for (int x = 0; x < CF::N; ++x) {
-            const uint32_t v = rand_masked(mt, RNGT) + 1u;
-            if (mask.test(x)) set_cell<CF, CF::BITS>(P, x, (int)v);
-        }
-    }
+    while (!mt.overflow && get_match_mask<CF>(P, mask)) fill(&mask);  // :23-27
 }
 
 // --------------------------------------------------------------------------

@@ -33,9 +33,11 @@ EXPORTS = [
     "m3_abi_version", "m3_last_error", "m3_device_count", "m3_supported", "m3_action_space",
     "m3_ctx_create", "m3_ctx_destroy", "m3_ctx_synchronize",
     "m3_init_boards", "m3_apply_actions", "m3_legal_actions",
-    "m3_env_create", "m3_env_destroy", "m3_env_reset", "m3_env_set_autoreset", "m3_env_step",
+    "m3_env_create", "m3_env_destroy", "m3_env_reset", "m3_env_set_shards", "m3_env_synchronize",
+    "m3_env_set_autoreset", "m3_env_step",
     "m3_env_step_device", "m3_env_get", "m3_env_device_ptr",
-    "m3_comm_unique_id", "m3_env_comm_init", "m3_env_gather", "m3_env_timing", "m3_env_kernel_ms",
+    "m3_comm_unique_id", "m3_env_comm_init", "m3_env_gather", "m3_env_stats", "m3_env_timing",
+    "m3_env_kernel_ms",
 ]
 
 
@@ -77,6 +79,8 @@ def lib():
             "m3_env_create": ([vp, i64, i32, i32, vp], i32),
             "m3_env_destroy": ([vp], i32),
             "m3_env_reset": ([vp, vp, u32], i32),
+            "m3_env_set_shards": ([vp, i32], i32),
+            "m3_env_synchronize": ([vp], i32),
             "m3_env_set_autoreset": ([vp, i32, u32], i32),
             "m3_env_step": ([vp, vp], i32),
             "m3_env_step_device": ([vp, vp], i32),
@@ -85,6 +89,7 @@ def lib():
             "m3_comm_unique_id": ([vp], i32),
             "m3_env_comm_init": ([vp, vp, i32, i32], i32),
             "m3_env_gather": ([vp, vp], i32),
+            "m3_env_stats": ([vp, vp], i32),
             "m3_env_timing": ([vp, i32], i32),
             "m3_env_kernel_ms": ([vp, vp, i32, vp], i32),
         }

@@ -33,7 +33,7 @@ from ._native import check, lib, ptr
 class BatchedMatch3Env:
     def __init__(self, n: int, rows: int = 9, columns: int = 9, types: int = 6, num_moves: int = 20,
                  env_goal: int = 500, device: int = 0, seeds=None, seed_base: int = 1,
-                 autoreset: bool = True, seed_stride: int = None):
+                 autoreset: bool = True, seed_stride: int = None, shards: int = None):
         self.n = int(n)
         self.rows, self.columns, self.types = rows, columns, types
         self.num_moves, self.env_goal = num_moves, env_goal
@@ -44,6 +44,8 @@ class BatchedMatch3Env:
         self.handle = h
         stride = self.n if seed_stride is None else int(seed_stride)
         self.set_autoreset(autoreset, stride)
+        if shards is not None:
+            self.set_shards(shards)
         self.reset(seeds=seeds, seed_base=seed_base)
 
     # ---- lifecycle -------------------------------------------------------------------
@@ -88,7 +90,11 @@ class BatchedMatch3Env:
         check(lib().m3_env_step_device(self.handle, device_actions_ptr))
 
     def synchronize(self):
-        check(lib().m3_ctx_synchronize(self.ctx.handle))
+        check(lib().m3_env_synchronize(self.handle))
+
+    def set_shards(self, nshards: int):
+        """Number of independent board shards / HIP streams (1..8); results do not depend on it."""
+        check(lib().m3_env_set_shards(self.handle, int(nshards)))
 
     def enable_timing(self, capacity: int):
         """Record HIP events around the next `capacity` step-kernel launches."""
@@ -101,6 +107,13 @@ class BatchedMatch3Env:
         n = ctypes.c_int(0)
         check(lib().m3_env_kernel_ms(self.handle, ptr(out), cap, ctypes.byref(n)))
         return out[: n.value].copy()
+
+    def stats(self) -> dict:
+        """Cumulative counters since reset (exact-fallback recomputes, autoresets, shards)."""
+        out = np.zeros(4, np.uint64)
+        check(lib().m3_env_stats(self.handle, ptr(out)))
+        return dict(step_recomputes=int(out[0]), reset_recomputes=int(out[1]), autoresets=int(out[2]),
+                    shards=int(out[3]))
 
     # ---- copy-outs ------------------------------------------------------------------
     def _get(self, what, dtype, shape):

@@ -96,6 +96,14 @@ int m3_env_destroy(m3_env *env);
  * NULL for seeds seed_base + i. Draws each board's first seeded random action. */
 int m3_env_reset(m3_env *env, const uint32_t *seeds, uint32_t seed_base);
 
+/* Split the boards into nshards (1..8) contiguous shards, each stepped on its
+ * own HIP stream; a shard's small, latency-bound autoreset launch then
+ * overlaps the other shards' step kernels. Results do not depend on it.
+ * Default: one shard per 262,144 boards, at most 4. */
+int m3_env_set_shards(m3_env *env, int nshards);
+/* Wait for all work of the env (every shard stream). */
+int m3_env_synchronize(m3_env *env);
+
 /* After a step, boards that are done are reset in place with seed += stride
  * (gymnasium vector-env autoreset; same-step semantics). Default: off. */
 int m3_env_set_autoreset(m3_env *env, int enabled, uint32_t seed_stride);
@@ -130,6 +138,12 @@ int m3_env_comm_init(m3_env *env, const uint8_t id[128], int nranks, int rank);
  * board of every rank into a device buffer [nranks][n]; optionally copied to
  * host_out (int32[nranks*n]). Enqueued on the env's stream. */
 int m3_env_gather(m3_env *env, int32_t *host_out);
+
+/* Cumulative counters since the last m3_env_reset: out[0] steps recomputed on
+ * the exact fallback pass (>= 624 MT draws or more match groups than the LDS
+ * table), out[1] resets recomputed by the wave-cooperative pass (>= 624 draws),
+ * out[2] autoresets, out[3] number of shards. */
+int m3_env_stats(m3_env *env, uint64_t out[4]);
 
 /* ---- timing helpers for bench.py ---------------------------------------- */
 /* Kernel-side timing: after m3_env_timing(env, cap), each of the next cap

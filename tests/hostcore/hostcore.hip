@@ -23,51 +23,87 @@ static void store_planes(const typename CF::Bd* P, int8_t* b) {
     memcpy(b, cw, CF::N);
 }
 
-template <class CF>
-static void apply_n(long n, const int8_t* boards, const uint32_t* seeds, const int32_t* nact, const int32_t* acts,
-                    int8_t* out, int32_t* rew, int32_t* draws, int32_t* flags, uint32_t* legal, int32_t* next_act) {
-    for (long i = 0; i < n; ++i) {
-        typename CF::Bd P[CF::NP], HL, VL;
-        load_planes<CF>(boards + i * CF::N, P);
-        ChainMT rng;
-        rng.init(seeds[i], mt_state397(seeds[i]));
-        uint32_t f;
-        int r = apply_action<CF>(P, nact[i], acts[i], rng, f, HL, VL);
-        if (f & FLAG_RNG_OVERFLOW) {
-            FullMT* fm = new FullMT;
-            load_planes<CF>(boards + i * CF::N, P);
-            fm->init(seeds[i], 0);
-            r = apply_action<CF>(P, nact[i], acts[i], *fm, f, HL, VL);
-            draws[i] = (int32_t)fm->k;
-            uint32_t act[CF::AW];
-            action_bits<CF>(HL, VL, act);
-            if (legal) memcpy(legal + i * CF::AW, act, sizeof(act));
-            next_act[i] = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act, *fm);
-            delete fm;
-            f |= FLAG_RNG_OVERFLOW;
-        } else {
-            draws[i] = (int32_t)rng.k;
-            uint32_t act[CF::AW];
-            action_bits<CF>(HL, VL, act);
-            if (legal) memcpy(legal + i * CF::AW, act, sizeof(act));
-            next_act[i] = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act, rng);
-        }
-        rew[i] = r;
-        flags[i] = (int32_t)f;
-        store_planes<CF>(P, out + i * CF::N);
+// One apply_action + next random action, the way the kernels do it: fast
+// path first (ChainMT + a group table of capacity CAP), full recompute
+// (FullMT + ArrayStore) when the fast path reports overflow.
+template <class CF, class Store>
+static int step_one(typename CF::Bd* P, const int8_t* board, uint32_t seed, int na, int act, Store& st,
+                    uint32_t& f, int32_t& draws, uint32_t* legal, int32_t& next_act, int& recomputed) {
+    typename CF::Bd HL, VL;
+    ChainMT rng;
+    rng.init(seed, mt_state397(seed));
+    int r = apply_action<CF>(P, na, act, rng, f, HL, VL, st);
+    uint32_t act_bits[CF::AW];
+    if (f & FLAG_RECOMPUTE) {
+        recomputed++;
+        FullMT* fm = new FullMT;
+        ArrayStore<CF>* as = new ArrayStore<CF>;
+        load_planes<CF>(board, P);
+        fm->init(seed, 0);
+        r = apply_action<CF>(P, na, act, *fm, f, HL, VL, *as);
+        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)fm->k;
+        action_bits<CF>(HL, VL, act_bits);
+        next_act = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act_bits, *fm);
+        delete fm;
+        delete as;
+    } else {
+        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)rng.k;
+        action_bits<CF>(HL, VL, act_bits);
+        next_act = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act_bits, rng);
     }
+    if (legal) memcpy(legal, act_bits, sizeof(act_bits));
+    return r;
 }
 
 template <class CF>
-static void init_n(long n, const uint32_t* seeds, int8_t* out, int32_t* draws, uint32_t* m397, int32_t* first_act) {
+static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const int32_t* nact, const int32_t* acts,
+                   int8_t* out, int32_t* rew, int32_t* draws, int32_t* flags, uint32_t* legal, int32_t* next_act,
+                   int small) {
+    int recomputed = 0;
+    for (long i = 0; i < n; ++i) {
+        typename CF::Bd P[CF::NP];
+        load_planes<CF>(boards + i * CF::N, P);
+        uint32_t f;
+        uint32_t* lg = legal ? legal + i * CF::AW : nullptr;
+        if (small == 8) {  // the 9x9 device table size
+            SmallStore<CF, 8> ss;
+            rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
+                                  next_act[i], recomputed);
+        } else if (small) {
+            SmallStore<CF, 1> ss;
+            rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
+                                  next_act[i], recomputed);
+        } else {
+            ArrayStore<CF>* as = new ArrayStore<CF>;
+            rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], *as, f, draws[i], lg,
+                                  next_act[i], recomputed);
+            delete as;
+        }
+        flags[i] = (int32_t)(f & ~FLAG_RECOMPUTE);
+        store_planes<CF>(P, out + i * CF::N);
+    }
+    return recomputed;
+}
+
+// BoardV2.__init__ the way k_init does it: ChainMT first, FullMT on overflow.
+template <class CF>
+static int init_n(long n, const uint32_t* seeds, int8_t* out, int32_t* draws, uint32_t* m397, int32_t* first_act) {
+    int recomputed = 0;
     for (long i = 0; i < n; ++i) {
         typename CF::Bd P[CF::NP], HL, VL;
-        FullMT* fm = new FullMT;
-        fm->init(seeds[i], 0);
-        m397[i] = fm->key[397];
-        init_board<CF>(P, *fm);
-        draws[i] = (int32_t)fm->k;
-        delete fm;
+        m397[i] = mt_state397(seeds[i]);
+        ChainMT cm;
+        cm.init(seeds[i], m397[i]);
+        init_board<CF>(P, cm);
+        draws[i] = (int32_t)cm.k;
+        if (cm.overflow) {
+            recomputed++;
+            FullMT* fm = new FullMT;
+            fm->init(seeds[i], 0);
+            init_board<CF>(P, *fm);
+            draws[i] = (int32_t)fm->k;
+            delete fm;
+        }
         legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
         uint32_t act[CF::AW];
         action_bits<CF>(HL, VL, act);
@@ -76,6 +112,7 @@ static void init_n(long n, const uint32_t* seeds, int8_t* out, int32_t* draws, u
         first_act[i] = random_action<CF>(act, rng);
         store_planes<CF>(P, out + i * CF::N);
     }
+    return recomputed;
 }
 
 template <class CF>
@@ -93,7 +130,9 @@ static void matches_n(long n, const int8_t* tbs, uint8_t* mask, int32_t* spawn, 
     for (long i = 0; i < n; ++i) {
         typename CF::Bd P[CF::NP], mk, sw[3];
         load_planes<CF>(tbs + i * CF::N, P);
-        found[i] = get_matches<CF, true>(P, mk, sw);
+        ArrayStore<CF>* as = new ArrayStore<CF>;
+        found[i] = get_matches<CF>(P, mk, sw, *as);
+        delete as;
         for (int x = 0; x < CF::N; ++x) {
             mask[i * CF::N + x] = (uint8_t)mk.test(x);
             int v = (int)sw[0].test(x) * CF::H + (int)sw[1].test(x) * CF::V + (int)sw[2].test(x) * CF::M;
@@ -120,17 +159,19 @@ using C16 = Cfg<16, 16, 8>;
 
 extern "C" {
 int hc_apply(int cfg, long n, const int8_t* b, const uint32_t* s, const int32_t* na, const int32_t* a, int8_t* o,
-             int32_t* r, int32_t* d, int32_t* f, uint32_t* legal, int32_t* next_act) {
-#define CALL(CF) apply_n<CF>(n, b, s, na, a, o, r, d, f, legal, next_act)
+             int32_t* r, int32_t* d, int32_t* f, uint32_t* legal, int32_t* next_act, int small) {
+    int rc = 0;
+#define CALL(CF) rc = apply_n<CF>(n, b, s, na, a, o, r, d, f, legal, next_act, small)
     DISPATCH(cfg, CALL);
 #undef CALL
-    return 0;
+    return rc;
 }
 int hc_init(int cfg, long n, const uint32_t* s, int8_t* o, int32_t* d, uint32_t* m397, int32_t* fa) {
-#define CALL(CF) init_n<CF>(n, s, o, d, m397, fa)
+    int rc = 0;
+#define CALL(CF) rc = init_n<CF>(n, s, o, d, m397, fa)
     DISPATCH(cfg, CALL);
 #undef CALL
-    return 0;
+    return rc;
 }
 int hc_legal(int cfg, long n, const int8_t* b, uint32_t* out) {
 #define CALL(CF) legal_n<CF>(n, b, out)

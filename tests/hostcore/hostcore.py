@@ -44,7 +44,7 @@ class HostCore:
         self.N = R * C
         self.aw = AW[(R, C, T)]
 
-    def apply(self, boards, seeds, n_actions, actions):
+    def apply(self, boards, seeds, n_actions, actions, small=False):
         boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
         n = len(boards)
         seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
@@ -53,8 +53,8 @@ class HostCore:
         out = np.zeros_like(boards)
         rew = np.zeros(n, np.int32); drw = np.zeros(n, np.int32); flg = np.zeros(n, np.int32)
         legal = np.zeros((n, self.aw), np.uint32); nxt = np.zeros(n, np.int32)
-        lib().hc_apply(self.cfg, ctypes.c_long(n), _p(boards), _p(seeds), _p(na), _p(acts), _p(out), _p(rew),
-                       _p(drw), _p(flg), _p(legal), _p(nxt))
+        self.recomputed = lib().hc_apply(self.cfg, ctypes.c_long(n), _p(boards), _p(seeds), _p(na), _p(acts),
+                                         _p(out), _p(rew), _p(drw), _p(flg), _p(legal), _p(nxt), int(small))
         return out, rew, drw, flg, legal, nxt
 
     def init(self, seeds):
@@ -62,7 +62,7 @@ class HostCore:
         n = len(seeds)
         out = np.zeros((n, self.N), np.int8); drw = np.zeros(n, np.int32)
         m397 = np.zeros(n, np.uint32); fa = np.zeros(n, np.int32)
-        lib().hc_init(self.cfg, ctypes.c_long(n), _p(seeds), _p(out), _p(drw), _p(m397), _p(fa))
+        self.recomputed = lib().hc_init(self.cfg, ctypes.c_long(n), _p(seeds), _p(out), _p(drw), _p(m397), _p(fa))
         return out, drw, m397, fa
 
     def legal(self, boards):

@@ -196,3 +196,36 @@ def test_edge_inputs(ctxs):
         for i in (0, n // 2, n - 1):
             ob, orr, od, _ = o.apply_action(bb[i].astype(np.int32), int(seeds[i]), int(fa[i]))
             assert (r["boards"][i] == ob).all() and r["reward"][i] == orr and r["draws"][i] == od
+
+
+def test_shards_do_not_change_results():
+    """Boards split over 1, 3 or 8 HIP streams step identically (autoreset on, env_goal 500)."""
+    n = 300_000
+    outs = []
+    for shards in (1, 3, 8):
+        env = BatchedMatch3Env(n, num_moves=20, env_goal=500, seed_base=7, autoreset=True, shards=shards)
+        acc = np.zeros(n, np.int64)
+        for _ in range(25):
+            env.step()
+            acc = acc * 3 + env.rewards()
+        outs.append((env.observations().copy(), acc, env.seeds().copy(), env.next_actions().copy()))
+        env.close()
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert (x == y).all()
+
+
+def test_explicit_actions_match_stateless_apply():
+    """env.step(actions) == BoardV2.apply_action on the same boards (host actions path)."""
+    n = 4096
+    env = BatchedMatch3Env(n, num_moves=20, env_goal=BIG, seed_base=11, autoreset=False, shards=2)
+    ctx = env.ctx
+    rng = np.random.default_rng(3)
+    for m in range(5):
+        obs = env.observations()
+        acts = rng.integers(0, 144, size=n).astype(np.int32)
+        ref = ctx.apply_actions(obs, env.seeds(), 20 - m, acts)
+        env.step(acts)
+        assert (env.observations() == ref["boards"]).all()
+        assert (env.rewards() == ref["reward"]).all()
+    env.close()

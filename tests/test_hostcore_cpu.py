@@ -85,3 +85,26 @@ def test_random_states_vs_oracle():
         bits = np.zeros(144, np.uint8)
         bits[o.legal_actions(ob)] = 1
         assert (np.unpackbits(legal[i].view(np.uint8), bitorder="little")[:144] == bits).all()
+
+
+@pytest.mark.parametrize("tag", list(SHAPES))
+def test_group_overflow_fallback_is_exact(golden, tag):
+    """A 1-group table overflows on every multi-group match; the recompute must give identical results."""
+    hc = HostCore(*SHAPES[tag])
+    st = golden("steps")
+    args = (st["board_" + tag], st["seed_" + tag], st["n_actions_" + tag], st["action_" + tag])
+    a = hc.apply(*args)
+    b = hc.apply(*args, small=True)
+    assert hc.recomputed > 10
+    for x, y in zip(a, b):
+        assert (x == y).all()
+
+
+def test_chain_init_fallback_counts(golden):
+    """Reset runs on the register-only MT19937 chain; seeds needing >= 624 draws are recomputed exactly."""
+    for tag in SHAPES:
+        hc = HostCore(*SHAPES[tag])
+        ini = golden("init")
+        out, drw, _, _ = hc.init(ini["seeds_" + tag])
+        assert (out == ini["boards_" + tag].reshape(len(out), -1)).all() and (drw == ini["draws_" + tag]).all()
+        assert hc.recomputed == int((ini["draws_" + tag] > 623).sum())
