@@ -72,10 +72,21 @@ constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 
 // Per-shape step-kernel geometry: boards (lanes) per workgroup and the
 // match-group table capacity, sized so staging + table fit the 160 KB LDS.
+// One wave per workgroup: the boards of a wave are staged through its own LDS
+// slice, so a wave that finishes early never waits at a barrier for the
+// workgroup's slowest wave (cascade depth varies a lot between boards) and its
+// slot is refilled at once.
 template <class CF>
 struct KS {
-    static constexpr int B = CF::N > 128 ? 128 : 256;
+    static constexpr int B = 64;
     static constexpr int GCAP = CF::N > 128 ? 4 : 8;
+    // per-board stream cache of the batched env (m3_rules.hpp, StreamCache)
+    using SC = StreamCache<CF>;
+    static constexpr int RAWN = SC::RAWN, ACCW = SC::ACCW, TSW = SC::TSW;
+    using RawT = typename SC::RawT;
+    static constexpr int TS_WORDS = CF::BITS * TSW;                 // per board in HBM
+    static constexpr int LDS_WORDS = CF::BITS * (TSW + 1) + ACCW;   // per lane in LDS (+ zero pad per plane)
+    using Rng = typename SC::Rng;
 };
 
 // Per-lane match-group table in LDS (see m3_rules.hpp, match_scan). Entry
@@ -109,6 +120,45 @@ struct LdsStore {
     }
 };
 
+// Phase profiling (profiling build only, -DM3_PHASE_PROF; tools/phase_prof.py).
+// mark<K>() charges the wave's cycles since the previous mark to phase K; the
+// first active lane keeps the per-wave accumulators in LDS, so the split is
+// exact wave time even inside divergent loops.
+#ifdef M3_PHASE_PROF
+constexpr int PROF_SLOTS = PH_N + 2;  // phases, total cycles, waves
+__device__ unsigned long long g_prof[2][PROF_SLOTS];  // [0] k_env_step, [1] k_init
+template <class Base>
+struct Prof : Base {
+    static constexpr bool PROF = true;
+    unsigned long long* w;  // this wave's LDS slot: PH_N accumulators, last, start
+    template <int K>
+    __device__ __forceinline__ void mark() {
+        const unsigned long long now = clock64();
+        if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) {
+            w[K] += now - w[PH_N];
+            w[PH_N] = now;
+        }
+    }
+    __device__ __forceinline__ void begin() {
+        if (__lane_id() == 0) {
+            for (int k = 0; k < PH_N; ++k) w[k] = 0;
+            w[PH_N] = w[PH_N + 1] = clock64();
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    __device__ __forceinline__ void end(int which) {
+        mark<PH_STORE>();
+        __builtin_amdgcn_wave_barrier();
+        if (__lane_id() == 0) {
+            for (int k = 0; k < PH_N; ++k) atomicAdd(&g_prof[which][k], w[k]);
+            atomicAdd(&g_prof[which][PH_N], w[PH_N] - w[PH_N + 1]);
+            atomicAdd(&g_prof[which][PH_N + 1], 1ull);
+        }
+    }
+};
+#define M3_PROF_LDS(LANES) __shared__ unsigned long long prof_s[(LANES) / 64][PH_N + 2];
+#endif
+
 // ---------------------------------------------------------------------------
 // LDS staging
 // ---------------------------------------------------------------------------
@@ -130,6 +180,32 @@ __device__ __forceinline__ void block_copy_out(int8_t* __restrict__ g, const uin
     uint4* d4 = reinterpret_cast<uint4*>(g);
     for (int i = threadIdx.x; i < n16; i += BLOCK) d4[i] = s4[i];
     for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) g[i] = (int8_t)lds[i];
+}
+
+// N cell bytes (little-endian in cw[ceil(N/4)]) to dst of any alignment:
+// up to 3 head bytes, aligned dwords (one funnel shift each), up to 3 tail
+// bytes -- instead of N byte stores.
+template <int N>
+__device__ __forceinline__ void store_cells(uint8_t* dst, const uint32_t* cw) {
+    constexpr int NW = (N + 3) / 4;
+    const uint32_t head = (4u - ((uint32_t)(uintptr_t)dst & 3u)) & 3u;
+    const uint32_t nd = ((uint32_t)N - head) >> 2;
+    const uint32_t t0 = head + 4u * nd;
+    const uint32_t s = 8u * head;
+#pragma unroll
+    for (int y = 0; y < 3; ++y)
+        if ((uint32_t)y < head) dst[y] = (uint8_t)(cw[y >> 2] >> (8 * (y & 3)));
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        if ((uint32_t)i < nd) {
+            const uint32_t lo = cw[i], hi = (i + 1 < NW) ? cw[i + 1] : 0u;
+            d32[i] = s ? ((lo >> s) | (hi << (32u - s))) : lo;
+        }
+    }
+#pragma unroll
+    for (int y = N - 3; y < N; ++y)
+        if ((uint32_t)y >= t0) dst[y] = (uint8_t)(cw[y >> 2] >> (8 * (y & 3)));
 }
 
 // lane's board (N bytes at lds + slot*N, any alignment) -> bit-planes.
@@ -157,8 +233,7 @@ __device__ __forceinline__ void planes_to_bytes(const typename CF::Bd* P, uint8_
     constexpr int NW = (CF::N + 3) / 4;
     uint32_t cw[NW];
     words_from_planes<CF>(P, cw);
-#pragma unroll
-    for (int x = 0; x < CF::N; ++x) dst[x] = (uint8_t)(cw[x >> 2] >> (8 * (x & 3)));
+    store_cells<CF::N>(dst, cw);
 }
 
 template <class CF>
@@ -214,14 +289,16 @@ __device__ __forceinline__ bool apply_and_emit(typename CF::Bd* P, const ApplyAr
     if (f & FLAG_RECOMPUTE) return false;
     const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
     a.reward[b] = r;
-    a.draws[b] = stepped ? rng.k : 0u;
+    a.draws[b] = stepped ? rng.draws() : 0u;
     uint32_t act[CF::AW];
     action_bits<CF>(HL, VL, act);
     int na = -1;
     if (stepped) {
         na = random_action<CF>(act, rng);
+        if (rng.overflow) return false;
         if (na < 0) f |= FLAG_NO_LEGAL;
     }
+    mark<PH_NEXT>(st);
     a.flags[b] = f;
     if (a.next_action) a.next_action[b] = na;
     if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
@@ -294,6 +371,12 @@ struct InitArgs {
     uint32_t* flags;         // nullable
     uint32_t* ovf_count;     // boards whose init needed >= 624 draws (FullMT recompute)
     uint32_t* ovf_list;
+    // nullable: env stream cache (KS<CF>): raw rows [b][RAWN], tile planes and
+    // acceptance words SoA with board stride cstride
+    void* sraw;
+    uint32_t* sts;
+    uint32_t* sacc;
+    int64_t cstride;
 };
 
 // BoardV2.__init__ (boardv2.py:17-27) + first seeded random action
@@ -323,16 +406,36 @@ __device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, uint3
     if (a.flags) a.flags[b] = fa < 0 ? FLAG_NO_LEGAL : 0u;
 }
 
-template <class CF, class RNG>
-__device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t m397, RNG& mt) {
+// Reset of board b on a tile stream generated in LDS (init_board_tiles); with
+// the env's cache pointers set it also writes the step's stream cache.
+// Returns false if the reset needs >= 624 draws (k_init_fix redoes it).
+template <class CF, class S = NoStore>
+__device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t m397, uint32_t* tm,
+                                          S* ps = nullptr) {
+    using K = KS<CF>;
+    using RawT = typename K::RawT;
+    constexpr int TW = TileGen<CF>::TWMAX;
     typename CF::Bd P[CF::NP];
-    init_board<CF>(P, mt);
-    if (mt.overflow) return false;
-    init_outputs<CF>(a, b, seed, m397, mt.k, P);
-    uint8_t tmp[CF::N];
-    planes_to_bytes<CF>(P, tmp);
-    int8_t* dst = a.boards + b * CF::N;
-    for (int x = 0; x < CF::N; ++x) dst[x] = (int8_t)tmp[x];
+    ChainMT g;
+    g.init(seed, m397);
+    RawT* row = a.sraw ? static_cast<RawT*>(a.sraw) + b * K::RAWN : nullptr;
+    uint32_t draws = 0;
+    const bool ok = init_board_tiles<CF>(
+        P, g, tm, INIT_BLOCK, draws, a.sraw ? (uint32_t)K::RAWN : 0u,
+        [&](uint32_t k, uint32_t v) { row[k] = (RawT)v; },
+        [&](uint32_t w, uint32_t v) { a.sacc[(int64_t)w * a.cstride + b] = v; }, ps);
+    if (a.sts) {
+#pragma unroll
+        for (int p = 0; p < CF::BITS; ++p)
+#pragma unroll
+            for (int w = 0; w < K::TSW; ++w) a.sts[(int64_t)(p * K::TSW + w) * a.cstride + b] = tm[(p * TW + w) * INIT_BLOCK];
+    }
+    if (!ok) return false;
+    init_outputs<CF>(a, b, seed, m397, draws, P);
+    constexpr int NW = (CF::N + 3) / 4;
+    uint32_t cw[NW];
+    words_from_planes<CF>(P, cw);
+    store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.boards + b * CF::N), cw);
     return true;
 }
 
@@ -341,19 +444,36 @@ template <class CF>
 __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
     if (a.list_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.ovf_count + 8, (uint32_t)cnt);  // stats: resets
+    __shared__ uint32_t tm_s[CF::BITS * TileGen<CF>::TWMAX * INIT_BLOCK];
+    uint32_t* tm = tm_s + threadIdx.x;
+#ifdef M3_PHASE_PROF
+    M3_PROF_LDS(INIT_BLOCK)
+    Prof<NoStore> ps;
+    ps.w = prof_s[threadIdx.x >> 6];
+    const bool live = (int64_t)blockIdx.x * INIT_BLOCK < cnt;
+    if (live) ps.begin();
+#else
+    NoStore* const pp = nullptr;
+#endif
     for (int64_t i = (int64_t)blockIdx.x * INIT_BLOCK + threadIdx.x; i < cnt;
          i += (int64_t)gridDim.x * INIT_BLOCK) {
         const int64_t b = a.list ? (int64_t)a.list[i] : i;
         const uint32_t seed = a.seeds[b] + a.stride;
         if (a.seeds_out) a.seeds_out[b] = seed;
         const uint32_t m397 = mt_state397(seed);
-        ChainMT mt;
-        mt.init(seed, m397);
-        if (!init_emit<CF>(a, b, seed, m397, mt)) {
+#ifdef M3_PHASE_PROF
+        const bool ok = init_emit<CF>(a, b, seed, m397, tm, &ps);
+#else
+        const bool ok = init_emit<CF>(a, b, seed, m397, tm, pp);
+#endif
+        if (!ok) {
             const uint32_t slot = atomicAdd(a.ovf_count, 1u);
             a.ovf_list[slot] = (uint32_t)b;
         }
     }
+#ifdef M3_PHASE_PROF
+    if (live) ps.end(1);
+#endif
 }
 
 // ---- wave-cooperative reset for boards whose reset needs >= 624 draws ----
@@ -515,6 +635,10 @@ struct EnvArgs {
     uint32_t* counters;  // [0] overflow count, [1] reset count
     uint32_t* ovf_list;
     uint32_t* reset_list;
+    const void* sraw;    // stream cache (see InitArgs)
+    const uint32_t* sts;
+    const uint32_t* sacc;
+    int64_t cstride;
 };
 
 // Match3Env.step bookkeeping (env.py:48-56) around BoardV2.apply_action.
@@ -531,14 +655,16 @@ __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& 
     const int mv1 = mv + 1;
     const int tr = sc >= a.goal;                        // env.py:53
     const int dn = tr || mv1 == a.num_moves;            // env.py:54
-    a.draws[b] = stepped ? rng.k : 0u;
+    a.draws[b] = stepped ? rng.draws() : 0u;
     uint32_t act[CF::AW];
     action_bits<CF>(HL, VL, act);
     int na = -1;
     if (stepped) {
         na = random_action<CF>(act, rng);
+        if (rng.overflow) return false;
         if (na < 0) f |= FLAG_NO_LEGAL;
     }
+    mark<PH_NEXT>(st);
     a.score[b] = sc;
     a.moves[b] = mv1;
     a.reward[b] = r;
@@ -548,9 +674,15 @@ __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& 
     a.next_action[b] = na;
     if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
     if (a.packed) a.packed[b] = (r << 2) | (tr << 1) | dn;
-    if (dn && a.autoreset) {
-        const uint32_t slot = atomicAdd(&a.counters[1], 1u);
-        a.reset_list[slot] = (uint32_t)b;
+    if (a.autoreset) {  // append to the reset list: one atomic per wave, not per lane
+        const uint64_t m = __ballot(dn);
+        if (m) {
+            const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&a.counters[1], (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (dn) a.reset_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)b;
+        }
     }
     return true;
 }
@@ -559,18 +691,43 @@ template <class CF>
 __global__ void __launch_bounds__(KS<CF>::B) k_env_step(EnvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[KS<CF>::B * CF::N + 16];
     __shared__ uint32_t gtab[LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::WORDS];
+    using K = KS<CF>;
+    __shared__ uint32_t cache_s[K::LDS_WORDS * K::B];
     const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
     const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
     block_copy_in<CF::N, KS<CF>::B>(a.cur + b0 * CF::N, lds, nb);
-    __syncthreads();
     const int t = threadIdx.x;
+    if (t < nb) {  // this lane's tile planes (+ zero pad) and acceptance words, lane-interleaved
+        const int64_t b = b0 + t;
+#pragma unroll
+        for (int p = 0; p < CF::BITS; ++p) {
+#pragma unroll
+            for (int w = 0; w < K::TSW; ++w)
+                cache_s[(p * (K::TSW + 1) + w) * K::B + t] = a.sts[(int64_t)(p * K::TSW + w) * a.cstride + b];
+            cache_s[(p * (K::TSW + 1) + K::TSW) * K::B + t] = 0u;
+        }
+#pragma unroll
+        for (int w = 0; w < K::ACCW; ++w)
+            cache_s[(CF::BITS * (K::TSW + 1) + w) * K::B + t] = a.sacc[(int64_t)w * a.cstride + b];
+    }
+    __syncthreads();
+#ifdef M3_PHASE_PROF
+    M3_PROF_LDS(KS<CF>::B)
+    Prof<LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>> st;
+    st.tab = gtab + t;
+    st.w = prof_s[t >> 6];
+    const bool live = ((t & ~63) < nb);
+    if (live) st.begin();
+#else
+    LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};
+#endif
     if (t < nb) {
         const int64_t b = b0 + t;
         typename CF::Bd P[CF::NP];
         lds_to_planes<CF>(lds, t, P);
-        ChainMT rng;
-        rng.init(a.seeds[b], a.mt397[b]);
-        LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};
+        typename K::Rng rng;
+        rng.init(static_cast<const typename K::RawT*>(a.sraw) + b * K::RAWN, cache_s + t,
+                 cache_s + CF::BITS * (K::TSW + 1) * K::B + t, K::B);
         if (!env_step_one<CF>(P, a, b, rng, st)) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
             a.ovf_list[slot] = (uint32_t)b;
@@ -579,6 +736,9 @@ __global__ void __launch_bounds__(KS<CF>::B) k_env_step(EnvArgs a) {
     }
     __syncthreads();
     block_copy_out<CF::N, KS<CF>::B>(a.nxt + b0 * CF::N, lds, nb);
+#ifdef M3_PHASE_PROF
+    if (live) st.end(0);
+#endif
 }
 
 template <class CF>
@@ -647,6 +807,9 @@ struct m3_env {
     int32_t* actions = nullptr;
     uint32_t* counters = nullptr;
     uint32_t *ovf_list = nullptr, *reset_list = nullptr, *init_ovf_list = nullptr;
+    // per-board stream cache (KS<CF>): raw rows, tile planes, acceptance words
+    void* sraw = nullptr;
+    uint32_t *sts = nullptr, *sacc = nullptr;
     int32_t* packed = nullptr;
     int32_t* gathered = nullptr;
     ncclComm_t comm = nullptr;
@@ -770,6 +933,10 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.counters = cnt;
     a.ovf_list = e->ovf_list + o;
     a.reset_list = e->reset_list + o;
+    a.sraw = static_cast<const typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
+    a.sts = e->sts + o;
+    a.sacc = e->sacc + o;
+    a.cstride = e->n;
     HIP_TRY(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
     const bool timed = e->tn < e->tcap;
     if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], st));
@@ -797,6 +964,10 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.moves = e->moves + o;
         r.ovf_count = &cnt[2];
         r.ovf_list = e->init_ovf_list + o;
+        r.sraw = static_cast<typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
+        r.sts = e->sts + o;
+        r.sacc = e->sacc + o;
+        r.cstride = e->n;
         // reward/done/trunc/flags of the finished step stay visible; the grid
         // is sized for the expected number of finished boards and grid-strides
         int rc = launch_init<CF>(st, r, sh.n / 8 + 1);
@@ -1062,6 +1233,13 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     alloc(&e->reset_list, n * 4);
     alloc(&e->init_ovf_list, n * 4);
     alloc(&e->packed, n * 4);
+    with_shape(c->shape, [&](auto cf) {
+        using K = KS<decltype(cf)>;
+        alloc(&e->sraw, n * (size_t)K::RAWN * sizeof(typename K::RawT));
+        alloc(&e->sts, n * 4ull * K::TS_WORDS);
+        alloc(&e->sacc, n * 4ull * K::ACCW);
+        return 0;
+    });
     if (err == hipSuccess) err = hipEventCreateWithFlags(&e->gather_ev, hipEventDisableTiming);
     if (err != hipSuccess) {
         m3_env_destroy(e);
@@ -1117,7 +1295,8 @@ int m3_env_destroy(m3_env* e) {
     if (e->gather_ev) (void)hipEventDestroy(e->gather_ev);
     void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->mt397, e->flags, e->draws, e->legal,
                     e->score, e->moves, e->next_action, e->reward, e->done, e->trunc, e->actions,
-                    e->counters, e->ovf_list, e->reset_list, e->init_ovf_list, e->packed, e->gathered};
+                    e->counters, e->ovf_list, e->reset_list, e->init_ovf_list, e->packed, e->gathered,
+                    e->sraw, e->sts, e->sacc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (e->comm) ncclCommDestroy(e->comm);
@@ -1159,6 +1338,10 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     a.draws = e->draws;
     a.ovf_count = &e->counters[2];
     a.ovf_list = e->init_ovf_list;
+    a.sraw = e->sraw;
+    a.sts = e->sts;
+    a.sacc = e->sacc;
+    a.cstride = e->n;
     HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));  // also clears the stats
     int rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, e->n); });
     if (rc) return rc;
@@ -1291,6 +1474,19 @@ int m3_env_stats(m3_env* e, uint64_t out[4]) {
     out[3] = e->shards.size();
     return M3_OK;
 }
+
+#ifdef M3_PHASE_PROF
+// profiling build only (not part of include/m3.h): out[2][PH_N + 2]
+int m3_prof_read(uint64_t* out, int reset) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)));
+    if (reset) {
+        static const unsigned long long zero[2][PROF_SLOTS] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), zero, sizeof(zero)));
+    }
+    return PH_N;
+}
+#endif
 
 int m3_env_timing(m3_env* e, int capacity) {
     CHECK_ARG(e && capacity >= 0, "bad arguments");

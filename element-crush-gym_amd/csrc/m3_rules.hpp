@@ -17,10 +17,25 @@
 // Cross-references to the reference are file:line in each function.
 #pragma once
 
+#include <type_traits>
+
 #include "m3_bitboard.hpp"
 #include "m3_rng.hpp"
 
 namespace m3 {
+
+// Phase-profiling hooks. A Store type that defines PROF receives mark<K>() at
+// phase boundaries (m3_api.hip builds such a variant with -DM3_PHASE_PROF);
+// for every other Store the calls compile to nothing.
+enum : int { PH_LOAD, PH_SWAP, PH_MATCH, PH_CLEAR, PH_DROP, PH_REFILL, PH_LEGAL, PH_NEXT, PH_STORE, PH_N };
+template <class S, class = void>
+struct HasProf : std::false_type {};
+template <class S>
+struct HasProf<S, std::void_t<decltype(S::PROF)>> : std::true_type {};
+template <int K, class S>
+M3_HD void mark(S& st) {
+    if constexpr (HasProf<S>::value) st.template mark<K>();
+}
 
 constexpr int ceil_log2(int v) {
     int b = 0;
@@ -65,6 +80,19 @@ struct Cfg {
     static_assert(T >= 1 && BITS <= 4, "tile types must fit 4 bits");
     using Bd = BB<W>;
     using G = Geo<R, C, W>;
+};
+
+// Geometry of the batched env's per-board stream cache (m3_rng.hpp,
+// CachedRNG): RAWN raw outputs (RawT holds every mask a step applies: tiles
+// 2^BITS-1, shuffle <= 15, random action < 2^ceil(log2 A)), TSW words of tile
+// stream per plane, ACCW words of acceptance bitmap.
+template <class CF>
+struct StreamCache {
+    static constexpr int RAWN = CF::N > 128 ? 512 : 256;
+    static constexpr int ACCW = RAWN / 32;
+    static constexpr int TSW = CF::N > 128 ? 8 : 4;
+    using RawT = std::conditional_t<(CF::A > 256), uint16_t, uint8_t>;
+    using Rng = CachedRNG<RawT, RAWN, CF::BITS, TSW, ACCW>;
 };
 
 // --------------------------------------------------------------------------
@@ -520,8 +548,9 @@ M3_HD void merge_clip(typename CF::Bd* P, const typename CF::Bd& z, const typena
 
 // gravity + refill (:166-173). Columns left to right, new tiles on top in draw
 // order (new[0] at row 0). Tiles come from randint(1, T+1).
-template <class CF, class RNG>
-M3_HD void gravity_refill(typename CF::Bd* P, RNG& rng) {
+// gravity: returns the (top-aligned) empty cells
+template <class CF>
+M3_HD typename CF::Bd gravity(typename CF::Bd* P) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
     constexpr int C = CF::C, R = CF::R, NPU = 6;
@@ -545,7 +574,50 @@ M3_HD void gravity_refill(typename CF::Bd* P, RNG& rng) {
         }
         occ = occ.andnot(mv) | at<-C>(mv);
     }
-    Bd em = VALID.andnot(occ);              // top-aligned empty cells
+    return VALID.andnot(occ);
+}
+
+// Refill from a cached tile stream (CachedRNG): column c takes the next h_c
+// tiles, tile s_c + r going to row r (new[0] on top), so a column is one
+// funnel-shift extract per plane and a fixed deposit of its R bits -- no
+// MT19937, no rejection loop, no per-tile divergence.
+template <class CF, class RNG>
+M3_HD void refill_tiles(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng) {
+    using G = typename CF::G;
+    constexpr int C = CF::C, R = CF::R;
+    rng.begin_tiles();
+    uint32_t j = rng.j;
+    if (j + (uint32_t)em.popc() > rng.cap) {
+        rng.overflow = 1u;
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int h = (em & G::col_eq(c)).popc();
+        const uint32_t hm = (h >= 32) ? 0xFFFFFFFFu : ((1u << h) - 1u);
+#pragma unroll
+        for (int p = 0; p < CF::BITS; ++p) {
+            const uint32_t f = rng.tile_bits(p, j) & hm;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int x = r * C + c;
+                P[p].w[x >> 5] |= ((f >> r) & 1u) << (x & 31);
+            }
+        }
+        j += (uint32_t)h;
+    }
+    rng.j = j;
+}
+
+// refill of the top-aligned empty cells em
+template <class CF, class RNG>
+M3_HD void refill(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng) {
+    using Bd = typename CF::Bd;
+    constexpr int C = CF::C, R = CF::R;
+    if constexpr (HasTiles<RNG>::value) {
+        refill_tiles<CF>(P, em, rng);
+        return;
+    }
     if (!em.any()) return;
     uint32_t tops = em.w[0] & ((1u << C) - 1u);  // columns with at least one empty cell
     int c = __builtin_ctz(tops);
@@ -636,6 +708,7 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
     constexpr int H = CF::H, V = CF::V, B = CF::B, M = CF::M;
     constexpr Bd VALID = G::valid();
     flags = 0u;
+    mark<PH_LOAD>(st);
     if (n_actions < 1 || action < 0 || action >= CF::A) {      // :44-45, KeyError at :48
         flags = (n_actions < 1) ? FLAG_TERMINAL : FLAG_BAD_ACTION;
         legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
@@ -685,22 +758,30 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
     } else if (are(H, V)) {                                     // :130-132 rows < t.col, rows >= t.row
         zr = G::row_band(0, tc < R ? tc : R) | G::row_band(tr, R);
     } else {                                                    // :133-136
+        mark<PH_SWAP>(st);
         if (get_matches<CF>(P, zr, sw, st) == MATCH_OVERFLOW) {
             flags |= FLAG_GROUP_OVERFLOW;
             return 0;
         }
+        mark<PH_MATCH>(st);
     }
+    mark<PH_SWAP>(st);
     int reward = 0;
     // first pass with all 7 planes (input values may exceed 32 until the clip)
     Bd z = zr | VALID.andnot(tb_nonzero<CF>(P));
     z = fire_specials<CF, CF::NP>(P, z);
     reward += score<CF, CF::NP>(P, z);
     merge_clip<CF, CF::NP>(P, z, sw);
+    mark<PH_CLEAR>(st);
     for (;;) {                                                  // :138
-        gravity_refill<CF>(P, rng);                             // :166-173
+        const Bd em = gravity<CF>(P);                           // :166-173
+        mark<PH_DROP>(st);
+        refill<CF>(P, em, rng);
+        mark<PH_REFILL>(st);
         if (rng.overflow) break;
         Bd mask;
         int mr = get_matches<CF>(P, mask, sw, st);              // :176-181
+        mark<PH_MATCH>(st);
         if (mr == MATCH_OVERFLOW) {
             flags |= FLAG_GROUP_OVERFLOW;
             return 0;
@@ -725,12 +806,14 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
                 found = mr == MATCH_FOUND;
                 if (!found) legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
             }
+            mark<PH_LEGAL>(st);
             if (!found) break;                                   // :195-196
         }
         z = mask | VALID.andnot(tb_nonzero<CF>(P));            // :199 + TB==0 cells
         z = fire_specials<CF, 6>(P, z);
         reward += score<CF, 6>(P, z);
         merge_clip<CF, 6>(P, z, sw);
+        mark<PH_CLEAR>(st);
     }
     if (rng.overflow) flags |= FLAG_RNG_OVERFLOW;
     return reward;
@@ -740,8 +823,8 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
 // BoardV2.__init__ with array=None (boardv2.py:17-27). mt must be freshly
 // seeded. Writes the planes (values 1..T).
 // --------------------------------------------------------------------------
-template <class CF, class RNG>
-M3_HD void init_board(typename CF::Bd* P, RNG& mt) {
+template <class CF, class RNG, class S>
+M3_HD void init_board(typename CF::Bd* P, RNG& mt, S& st) {
     using Bd = typename CF::Bd;
 #pragma unroll
     for (int p = 0; p < CF::NP; ++p) P[p] = Bd::zero();
@@ -762,9 +845,133 @@ M3_HD void init_board(typename CF::Bd* P, RNG& mt) {
             ++x;
         }
     };
+    mark<PH_LOAD>(st);
     fill(nullptr);                                             // :21
+    mark<PH_REFILL>(st);
     Bd mask;
-    while (!mt.overflow && get_match_mask<CF>(P, mask)) fill(&mask);  // :23-27
+    for (;;) {                                                 // :23-27
+        if (mt.overflow) break;
+        const bool any = get_match_mask<CF>(P, mask);
+        mark<PH_MATCH>(st);
+        if (!any) break;
+        fill(&mask);
+        mark<PH_REFILL>(st);
+    }
+}
+
+template <class CF, class RNG>
+M3_HD void init_board(typename CF::Bd* P, RNG& mt) {
+    NoStore ns;
+    init_board<CF>(P, mt, ns);
+}
+
+// --------------------------------------------------------------------------
+// BoardV2.__init__ (boardv2.py:17-27) on a tile stream: every round of the
+// reference draws randint(1, T+1, (R, C)), i.e. the next N tiles of the
+// stream in row-major order, so a round is "take N tiles as bit-planes" (a
+// funnel shift of the stream's plane words) plus one masked merge. The
+// stream is generated as it is needed (one raw draw per loop trip, tiles
+// appended to plane words in `tm`, plane p word w at tm[(p*TWMAX + w)*stride]).
+// Raw outputs k < rawn and their acceptance bits go to the sinks, which is
+// exactly the step's stream cache (StreamCache), so a reset builds it for free.
+// Returns false if the board needs more than the first MT block (624 draws):
+// the caller recomputes it. `draws` = raw outputs consumed by __init__.
+// --------------------------------------------------------------------------
+template <class CF>
+struct TileGen {
+    static constexpr int TWMAX = 21;  // 624 tiles at most, + funnel pad
+};
+
+template <class CF, class RNG, class RawSink, class AccSink, class S = NoStore>
+M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, int stride, uint32_t& draws, uint32_t rawn,
+                            RawSink raw_sink, AccSink acc_sink, S* ps = nullptr) {
+    using Bd = typename CF::Bd;
+    using G = typename CF::G;
+    constexpr int TW = TileGen<CF>::TWMAX, N = CF::N;
+    constexpr Bd VALID = G::valid();
+    static_assert(CF::TILE_RNG > 0u, "randint(1, 2) consumes no draws");
+    uint32_t cur[CF::BITS];
+#pragma unroll
+    for (int p = 0; p < CF::BITS; ++p) cur[p] = 0u;
+    uint32_t nt = 0u, accw = 0u;
+    // append tiles until `target` exist (or, with raw_only, until rawn raw draws)
+    auto gen = [&](uint32_t target, bool raw_only) {
+        for (;;) {
+            const uint32_t k = g.k;
+            if (raw_only ? k >= rawn : nt >= target) break;
+            const uint32_t v = g.next32();
+            if (g.overflow) break;
+            const uint32_t t = v & CF::TILE_MASK;
+            const bool ok = t <= CF::TILE_RNG;
+            if (k < rawn) {
+                raw_sink(k, v);
+                accw |= (uint32_t)ok << (k & 31u);
+                if ((k & 31u) == 31u) {
+                    acc_sink(k >> 5, accw);
+                    accw = 0u;
+                }
+            }
+            if (ok && nt < (uint32_t)(32 * TW)) {
+                const uint32_t val = t + 1u, sh = nt & 31u;
+#pragma unroll
+                for (int p = 0; p < CF::BITS; ++p) cur[p] |= ((val >> p) & 1u) << sh;
+                ++nt;
+                if ((nt & 31u) == 0u) {
+#pragma unroll
+                    for (int p = 0; p < CF::BITS; ++p) {
+                        tm[(p * TW + (int)(nt >> 5) - 1) * stride] = cur[p];
+                        cur[p] = 0u;
+                    }
+                }
+            }
+        }
+        if ((nt >> 5) < (uint32_t)TW) {  // the partial word, so the round can read it
+#pragma unroll
+            for (int p = 0; p < CF::BITS; ++p) tm[(p * TW + (int)(nt >> 5)) * stride] = cur[p];
+        }
+    };
+    auto take = [&](uint32_t j, Bd* T) {  // tiles [j, j + N) as planes
+        const int q = (int)(j >> 5);
+        const uint32_t sh = j & 31u;
+#pragma unroll
+        for (int p = 0; p < CF::BITS; ++p) {
+            uint32_t lo = tm[(p * TW + q) * stride];
+#pragma unroll
+            for (int i = 0; i < CF::W; ++i) {
+                const uint32_t hi = (q + i + 1 < TW) ? tm[(p * TW + q + i + 1) * stride] : 0u;
+                T[p].w[i] = sh ? ((lo >> sh) | (hi << (32u - sh))) : lo;
+                lo = hi;
+            }
+            T[p] &= VALID;
+        }
+    };
+    if constexpr (HasProf<S>::value) ps->template mark<PH_LOAD>();
+#pragma unroll
+    for (int p = 0; p < CF::NP; ++p) P[p] = Bd::zero();
+    gen((uint32_t)N, false);                                   // :21
+    if (g.overflow) return false;
+    take(0u, P);
+    if constexpr (HasProf<S>::value) ps->template mark<PH_REFILL>();
+    uint32_t j = (uint32_t)N;
+    Bd mask;
+    for (;;) {                                                 // :23-27
+        const bool any = get_match_mask<CF>(P, mask);
+        if constexpr (HasProf<S>::value) ps->template mark<PH_MATCH>();
+        if (!any) break;
+        gen(j + (uint32_t)N, false);
+        if (g.overflow || j + (uint32_t)N > (uint32_t)(32 * TW)) return false;
+        Bd T[CF::BITS];
+        take(j, T);
+#pragma unroll
+        for (int p = 0; p < CF::BITS; ++p) P[p] = P[p].andnot(mask) | (T[p] & mask);
+        j += (uint32_t)N;
+        if constexpr (HasProf<S>::value) ps->template mark<PH_REFILL>();
+    }
+    draws = g.k;
+    gen(0u, true);  // complete the step's stream cache: raw draws [0, rawn)
+    if (rawn & 31u) acc_sink(rawn >> 5, accw);
+    if constexpr (HasProf<S>::value) ps->template mark<PH_NEXT>();
+    return true;
 }
 
 // --------------------------------------------------------------------------

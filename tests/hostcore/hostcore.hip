@@ -47,9 +47,73 @@ static int step_one(typename CF::Bd* P, const int8_t* board, uint32_t seed, int 
         delete fm;
         delete as;
     } else {
-        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)rng.k;
+        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)rng.draws();
         action_bits<CF>(HL, VL, act_bits);
         next_act = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act_bits, rng);
+    }
+    if (legal) memcpy(legal, act_bits, sizeof(act_bits));
+    return r;
+}
+
+// The batched-env path: stream cache built as at reset, CachedRNG for the
+// step, exact FullMT recompute when the cache or the group table overflows.
+template <class CF>
+static int step_cached(typename CF::Bd* P, const int8_t* board, uint32_t seed, int na, int act, uint32_t& f,
+                       int32_t& draws, uint32_t* legal, int32_t& next_act, int& recomputed) {
+    using SC = StreamCache<CF>;
+    typename SC::RawT raw[SC::RAWN], raw2[SC::RAWN];
+    uint32_t ts[CF::BITS * (SC::TSW + 1)], acc[SC::ACCW], ts2[CF::BITS * (SC::TSW + 1)], acc2[SC::ACCW];
+    // the cache as reset builds it (init_board_tiles) ...
+    {
+        static uint32_t tm[CF::BITS * TileGen<CF>::TWMAX];
+        memset(tm, 0, sizeof(tm));
+        typename CF::Bd Q[CF::NP];
+        ChainMT g;
+        g.init(seed, mt_state397(seed));
+        uint32_t d;
+        init_board_tiles<CF>(Q, g, tm, 1, d, (uint32_t)SC::RAWN,
+                             [&](uint32_t k, uint32_t v) { raw[k] = (typename SC::RawT)v; },
+                             [&](uint32_t w, uint32_t v) { acc[w] = v; });
+        for (int p = 0; p < CF::BITS; ++p) {
+            for (int w = 0; w < SC::TSW; ++w) ts[p * (SC::TSW + 1) + w] = tm[p * TileGen<CF>::TWMAX + w];
+            ts[p * (SC::TSW + 1) + SC::TSW] = 0u;
+        }
+    }
+    // ... must equal the straightforward construction
+    build_stream_cache<SC::RAWN, CF::BITS, SC::TSW, SC::ACCW, CF::TILE_MASK, CF::TILE_RNG>(
+        seed, mt_state397(seed), [&](int k, uint32_t v) { raw2[k] = (typename SC::RawT)v; },
+        [&](int p, int w, uint32_t v) { ts2[p * (SC::TSW + 1) + w] = v; }, [&](int w, uint32_t v) { acc2[w] = v; });
+    const uint32_t tiles = [&] { uint32_t c = 0; for (int w = 0; w < SC::ACCW; ++w) c += __builtin_popcount(acc2[w]); return c; }();
+    if (memcmp(raw, raw2, sizeof(raw)) || memcmp(acc, acc2, sizeof(acc))) recomputed += 1 << 20;  // flag: cache mismatch
+    for (int p = 0; p < CF::BITS; ++p)
+        for (uint32_t t = 0; t < tiles && t < (uint32_t)(32 * SC::TSW); ++t)
+            if (((ts[p * (SC::TSW + 1) + (t >> 5)] ^ ts2[p * (SC::TSW + 1) + (t >> 5)]) >> (t & 31)) & 1u)
+                recomputed += 1 << 20;
+    typename SC::Rng rng;
+    rng.init(raw, ts, acc, 1);
+    SmallStore<CF, 8> ss;
+    typename CF::Bd HL, VL;
+    int r = apply_action<CF>(P, na, act, rng, f, HL, VL, ss);
+    uint32_t act_bits[CF::AW];
+    bool redo = (f & FLAG_RECOMPUTE) != 0;
+    if (!redo) {
+        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)rng.draws();
+        action_bits<CF>(HL, VL, act_bits);
+        next_act = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act_bits, rng);
+        redo = rng.overflow != 0u;
+    }
+    if (redo) {
+        recomputed++;
+        FullMT* fm = new FullMT;
+        ArrayStore<CF>* as = new ArrayStore<CF>;
+        load_planes<CF>(board, P);
+        fm->init(seed, 0);
+        r = apply_action<CF>(P, na, act, *fm, f, HL, VL, *as);
+        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)fm->k;
+        action_bits<CF>(HL, VL, act_bits);
+        next_act = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act_bits, *fm);
+        delete fm;
+        delete as;
     }
     if (legal) memcpy(legal, act_bits, sizeof(act_bits));
     return r;
@@ -65,10 +129,23 @@ static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const in
         load_planes<CF>(boards + i * CF::N, P);
         uint32_t f;
         uint32_t* lg = legal ? legal + i * CF::AW : nullptr;
-        if (small == 8) {  // the 9x9 device table size
+        if (small == 16) {  // batched env path: stream cache + CachedRNG
+            rew[i] = step_cached<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], f, draws[i], lg,
+                                     next_act[i], recomputed);
+        } else if (small == 8) {  // the 9x9 device table size
             SmallStore<CF, 8> ss;
             rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
                                   next_act[i], recomputed);
+        } else if (small == 4 || small == 2) {  // candidate smaller device tables
+            if (small == 4) {
+                SmallStore<CF, 4> ss;
+                rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
+                                      next_act[i], recomputed);
+            } else {
+                SmallStore<CF, 2> ss;
+                rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
+                                      next_act[i], recomputed);
+            }
         } else if (small) {
             SmallStore<CF, 1> ss;
             rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
@@ -85,18 +162,21 @@ static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const in
     return recomputed;
 }
 
-// BoardV2.__init__ the way k_init does it: ChainMT first, FullMT on overflow.
+// BoardV2.__init__ the way k_init does it: tile stream on the ChainMT
+// (init_board_tiles), FullMT on overflow.
 template <class CF>
 static int init_n(long n, const uint32_t* seeds, int8_t* out, int32_t* draws, uint32_t* m397, int32_t* first_act) {
     int recomputed = 0;
+    static uint32_t tm[CF::BITS * TileGen<CF>::TWMAX];
     for (long i = 0; i < n; ++i) {
         typename CF::Bd P[CF::NP], HL, VL;
         m397[i] = mt_state397(seeds[i]);
         ChainMT cm;
         cm.init(seeds[i], m397[i]);
-        init_board<CF>(P, cm);
-        draws[i] = (int32_t)cm.k;
-        if (cm.overflow) {
+        uint32_t d = 0;
+        const bool ok = init_board_tiles<CF>(P, cm, tm, 1, d, 0u, [](uint32_t, uint32_t) {}, [](uint32_t, uint32_t) {});
+        draws[i] = (int32_t)d;
+        if (!ok) {
             recomputed++;
             FullMT* fm = new FullMT;
             fm->init(seeds[i], 0);
@@ -151,6 +231,34 @@ static void roundtrip_n(long n, const int8_t* boards, int8_t* out) {
     }
 }
 
+// Phase counter (profiling hook of m3_rules.hpp): how many cascade rounds a step runs.
+template <class CF>
+struct CountStore : ArrayStore<CF> {
+    static constexpr bool PROF = true;
+    int rounds = 0;
+    template <int K>
+    void mark() {
+        if (K == PH_REFILL) ++rounds;
+    }
+};
+
+template <class CF>
+static void rounds_n(long n, const int8_t* boards, const uint32_t* seeds, const int32_t* nact, const int32_t* acts,
+                     int32_t* rounds) {
+    for (long i = 0; i < n; ++i) {
+        typename CF::Bd P[CF::NP], HL, VL;
+        load_planes<CF>(boards + i * CF::N, P);
+        FullMT* fm = new FullMT;
+        fm->init(seeds[i], 0);
+        CountStore<CF>* cs = new CountStore<CF>;
+        uint32_t f;
+        apply_action<CF>(P, nact[i], acts[i], *fm, f, HL, VL, *cs);
+        rounds[i] = cs->rounds;
+        delete fm;
+        delete cs;
+    }
+}
+
 using C9 = Cfg<9, 9, 6>;
 using C16 = Cfg<16, 16, 8>;
 
@@ -187,6 +295,12 @@ int hc_matches(int cfg, long n, const int8_t* b, uint8_t* m, int32_t* sp, int32_
 }
 int hc_roundtrip(int cfg, long n, const int8_t* b, int8_t* o) {
 #define CALL(CF) roundtrip_n<CF>(n, b, o)
+    DISPATCH(cfg, CALL);
+#undef CALL
+    return 0;
+}
+int hc_rounds(int cfg, long n, const int8_t* b, const uint32_t* s, const int32_t* na, const int32_t* a, int32_t* r) {
+#define CALL(CF) rounds_n<CF>(n, b, s, na, a, r)
     DISPATCH(cfg, CALL);
 #undef CALL
     return 0;

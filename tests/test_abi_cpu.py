@@ -31,8 +31,9 @@ def test_library_exports_every_header_symbol():
 
 def test_no_torch_in_product_library():
     out = subprocess.run(["ldd", _native.LIB_PATH], capture_output=True, text=True).stdout
-    assert "torch" not in out and "c10" not in out
-    assert "libamdhip64" in out and "librccl" in out
+    libs = [line.split()[0] for line in out.splitlines() if line.strip()]  # names only, not load addresses
+    assert not [x for x in libs if "torch" in x or "c10" in x], libs
+    assert any("libamdhip64" in x for x in libs) and any("librccl" in x for x in libs), libs
 
 
 def test_loads_and_reports_shapes():
