@@ -411,7 +411,7 @@ __device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, uint3
 // Returns false if the reset needs >= 624 draws (k_init_fix redoes it).
 template <class CF, class S = NoStore>
 __device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t m397, uint32_t* tm,
-                                          S* ps = nullptr) {
+                                          uint32_t* pos, S* ps = nullptr) {
     using K = KS<CF>;
     using RawT = typename K::RawT;
     constexpr int TW = TileGen<CF>::TWMAX;
@@ -420,9 +420,17 @@ __device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t
     g.init(seed, m397);
     RawT* row = a.sraw ? static_cast<RawT*>(a.sraw) + b * K::RAWN : nullptr;
     uint32_t draws = 0;
+    constexpr uint32_t PER = 4u / sizeof(RawT), SH = 8u * sizeof(RawT);
+    uint32_t pk = 0u;  // PER raw entries per dword store (k is the same on every lane)
     const bool ok = init_board_tiles<CF>(
-        P, g, tm, INIT_BLOCK, draws, a.sraw ? (uint32_t)K::RAWN : 0u,
-        [&](uint32_t k, uint32_t v) { row[k] = (RawT)v; },
+        P, g, tm, pos, INIT_BLOCK, draws, a.sraw ? (uint32_t)K::RAWN : 0u,
+        [&](uint32_t k, uint32_t v) {
+            pk |= (v & ((1u << SH) - 1u)) << (SH * (k % PER));
+            if (k % PER == PER - 1u) {
+                reinterpret_cast<uint32_t*>(row)[k / PER] = pk;
+                pk = 0u;
+            }
+        },
         [&](uint32_t w, uint32_t v) { a.sacc[(int64_t)w * a.cstride + b] = v; }, ps);
     if (a.sts) {
 #pragma unroll
@@ -445,7 +453,9 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
     if (a.list_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.ovf_count + 8, (uint32_t)cnt);  // stats: resets
     __shared__ uint32_t tm_s[CF::BITS * TileGen<CF>::TWMAX * INIT_BLOCK];
+    __shared__ uint32_t pos_s[TileGen<CF>::MAXR * INIT_BLOCK];
     uint32_t* tm = tm_s + threadIdx.x;
+    uint32_t* pos = pos_s + threadIdx.x;
 #ifdef M3_PHASE_PROF
     M3_PROF_LDS(INIT_BLOCK)
     Prof<NoStore> ps;
@@ -462,9 +472,9 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
         if (a.seeds_out) a.seeds_out[b] = seed;
         const uint32_t m397 = mt_state397(seed);
 #ifdef M3_PHASE_PROF
-        const bool ok = init_emit<CF>(a, b, seed, m397, tm, &ps);
+        const bool ok = init_emit<CF>(a, b, seed, m397, tm, pos, &ps);
 #else
-        const bool ok = init_emit<CF>(a, b, seed, m397, tm, pp);
+        const bool ok = init_emit<CF>(a, b, seed, m397, tm, pos, pp);
 #endif
         if (!ok) {
             const uint32_t slot = atomicAdd(a.ovf_count, 1u);
@@ -644,14 +654,16 @@ struct EnvArgs {
 // Match3Env.step bookkeeping (env.py:48-56) around BoardV2.apply_action.
 template <class CF, class RNG, class Store>
 __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st) {
+    // every per-board input is loaded before the cascade, so its latency hides behind it
     const int act_in = a.actions ? a.actions[b] : a.next_action[b];
     const int mv = a.moves[b];
+    const int sc0 = a.score[b];
     typename CF::Bd HL, VL;
     uint32_t f;
     const int r = apply_action<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st);
     if (f & FLAG_RECOMPUTE) return false;
     const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
-    const int sc = a.score[b] + r;
+    const int sc = sc0 + r;
     const int mv1 = mv + 1;
     const int tr = sc >= a.goal;                        // env.py:53
     const int dn = tr || mv1 == a.num_moves;            // env.py:54

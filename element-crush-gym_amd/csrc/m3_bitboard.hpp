@@ -79,6 +79,23 @@ struct BB {
     }
 };
 
+M3_HD int select_bit(uint32_t u, int k) {  // position of the k-th (0-based) set bit of u
+    int pos = 0;
+#pragma unroll
+    for (int half = 16; half >= 1; half >>= 1) {
+        const uint32_t lo = u & ((1u << half) - 1u);
+        const int c = __builtin_popcount(lo);
+        if (k >= c) {
+            k -= c;
+            u >>= half;
+            pos += half;
+        } else {
+            u = lo;
+        }
+    }
+    return pos;
+}
+
 // out[y] = a[y + D]   (D > 0 looks "ahead" to higher cells, D < 0 looks back)
 template <int D, int W>
 M3_HD BB<W> at(const BB<W>& a) {

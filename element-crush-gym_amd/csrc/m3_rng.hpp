@@ -197,18 +197,27 @@ template <class RawT, int RAWN, int BITS, int TSW, int ACCW>
 struct CachedRNG {
     static constexpr bool TILES = true;
     static constexpr int TCAP = TSW * 32;
-    const RawT* raw;       // this board's RAWN-entry row
+    static constexpr uint32_t WE = 16u / sizeof(RawT);  // raw entries per 16-byte window
+    const RawT* raw;       // this board's RAWN-entry row (16-byte aligned)
     const uint32_t* ts;    // plane p, word w at ts[(p * (TSW + 1) + w) * stride] (word TSW is a zero pad)
     const uint32_t* acc;   // word w at acc[w * stride]
     int stride;
     uint32_t cap;          // tiles available: min(TCAP, accepted draws below RAWN)
     uint32_t kb, j, k, in_tiles, overflow;
+    uint32_t win[4], wlo;  // raw entries [wlo, wlo + WE), one 16-byte load
 
+    M3_HD void load_window(uint32_t at) {
+        wlo = at & ~(WE - 1u);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(raw + wlo);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) win[i] = src[i];
+    }
     M3_HD void init(const RawT* r, const uint32_t* t, const uint32_t* a, int st) {
         raw = r;
         ts = t;
         acc = a;
         stride = st;
+        load_window(0u);  // issued early: the random action usually reads the first few entries
         uint32_t n = 0;
 #pragma unroll
         for (int w = 0; w < ACCW; ++w) n += (uint32_t)__builtin_popcount(acc[w * stride]);
@@ -224,22 +233,20 @@ struct CachedRNG {
     }
     // raw position of the draw after the (jj-1)-th accepted one (jj >= 1)
     M3_HD uint32_t after_tile(uint32_t jj) const {
-        uint32_t rem = jj - 1u, pos = (uint32_t)RAWN;
+        uint32_t r = jj - 1u, word = 0u, wi = (uint32_t)ACCW;
         bool found = false;
 #pragma unroll
         for (int w = 0; w < ACCW; ++w) {
             const uint32_t a = acc[w * stride];
             const uint32_t c = (uint32_t)__builtin_popcount(a);
-            if (!found && rem < c) {
-                uint32_t x = a;
-                for (uint32_t i = 0; i < rem; ++i) x &= x - 1u;
-                pos = (uint32_t)(32 * w) + (uint32_t)__builtin_ctz(x);
-                found = true;
-            } else if (!found) {
-                rem -= c;
-            }
+            const bool here = !found && r < c;
+            word = here ? a : word;
+            wi = here ? (uint32_t)w : wi;
+            r = (found || here) ? r : r - c;
+            found = found || here;
         }
-        return pos + 1u;
+        if (!found) return (uint32_t)RAWN + 1u;
+        return 32u * wi + (uint32_t)select_bit(word, (int)r) + 1u;
     }
     M3_HD uint32_t draws() const {
         if (!in_tiles) return k;
@@ -256,7 +263,15 @@ struct CachedRNG {
             overflow = 1u;
             return 0u;
         }
-        return (uint32_t)raw[k++];
+        if (k - wlo >= WE) load_window(k);
+        const uint32_t e = k - wlo;
+        k += 1u;
+        constexpr uint32_t PER = 4u / sizeof(RawT), SH = 8u * sizeof(RawT);
+        const uint32_t q = e / PER;
+        uint32_t wv = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wv |= win[i] & (0u - (uint32_t)(q == (uint32_t)i));
+        return (wv >> (SH * (e % PER))) & ((1u << SH) - 1u);
     }
     // switch to tile mode at the current raw position
     M3_HD void begin_tiles() {

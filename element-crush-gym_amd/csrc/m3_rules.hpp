@@ -232,22 +232,6 @@ M3_HD void action_bits(const typename CF::Bd& HL, const typename CF::Bd& VL, uin
     action_bits_rows<CF, 0>(HL, VL, act);
 }
 
-M3_HD int select_bit(uint32_t u, int k) {  // position of the k-th (0-based) set bit of u
-    int pos = 0;
-#pragma unroll
-    for (int half = 16; half >= 1; half >>= 1) {
-        const uint32_t lo = u & ((1u << half) - 1u);
-        const int c = __builtin_popcount(lo);
-        if (k >= c) {
-            k -= c;
-            u >>= half;
-            pos += half;
-        } else {
-            u = lo;
-        }
-    }
-    return pos;
-}
 
 // np.random.choice(legal_actions) (samplerTasks.py:13): legal[randint(0, len)]
 template <class CF, class RNG>
@@ -774,41 +758,51 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
     merge_clip<CF, CF::NP>(P, z, sw);
     mark<PH_CLEAR>(st);
     for (;;) {                                                  // :138
-        const Bd em = gravity<CF>(P);                           // :166-173
-        mark<PH_DROP>(st);
-        refill<CF>(P, em, rng);
-        mark<PH_REFILL>(st);
-        if (rng.overflow) break;
         Bd mask;
-        int mr = get_matches<CF>(P, mask, sw, st);              // :176-181
-        mark<PH_MATCH>(st);
-        if (mr == MATCH_OVERFLOW) {
-            flags |= FLAG_GROUP_OVERFLOW;
-            return 0;
-        }
-        bool found = mr == MATCH_FOUND;
-        if (!found) {
-            legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
-            int shuffles = 0;
-            while (!found && !(HL.any() || VL.any())) {          // :188-194
-                if (shuffles >= CF::SHUFFLE_CAP) {
-                    flags |= FLAG_SHUFFLE_CAP;
-                    break;
-                }
-                shuffle_rows<CF>(P, rng);
-                flags |= FLAG_SHUFFLED;
-                ++shuffles;
-                mr = get_matches<CF>(P, mask, sw, st);
-                if (mr == MATCH_OVERFLOW) {
-                    flags |= FLAG_GROUP_OVERFLOW;
-                    return 0;
-                }
-                found = mr == MATCH_FOUND;
-                if (!found) legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
+        bool found = false;
+        for (;;) {  // cascade: refill, rematch, clear while matches remain
+            const Bd em = gravity<CF>(P);                       // :166-173
+            mark<PH_DROP>(st);
+            refill<CF>(P, em, rng);
+            mark<PH_REFILL>(st);
+            if (rng.overflow) break;
+            const int mr = get_matches<CF>(P, mask, sw, st);    // :176-181
+            mark<PH_MATCH>(st);
+            if (mr == MATCH_OVERFLOW) {
+                flags |= FLAG_GROUP_OVERFLOW;
+                return 0;
             }
-            mark<PH_LEGAL>(st);
-            if (!found) break;                                   // :195-196
+            if (mr != MATCH_FOUND) break;
+            z = mask | VALID.andnot(tb_nonzero<CF>(P));        // :199 + TB==0 cells
+            z = fire_specials<CF, 6>(P, z);
+            reward += score<CF, 6>(P, z);
+            merge_clip<CF, 6>(P, z, sw);
+            mark<PH_CLEAR>(st);
         }
+        if (rng.overflow) break;
+        // no match left: the legal set of the settled board, computed once
+        // after the (divergent) cascade so the wave runs it once
+        legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
+        mark<PH_LEGAL>(st);
+        if (HL.any() || VL.any()) break;
+        int shuffles = 0;                                       // :188-194 dead board
+        while (!found && !(HL.any() || VL.any())) {
+            if (shuffles >= CF::SHUFFLE_CAP) {
+                flags |= FLAG_SHUFFLE_CAP;
+                break;
+            }
+            shuffle_rows<CF>(P, rng);
+            flags |= FLAG_SHUFFLED;
+            ++shuffles;
+            const int mr = get_matches<CF>(P, mask, sw, st);
+            if (mr == MATCH_OVERFLOW) {
+                flags |= FLAG_GROUP_OVERFLOW;
+                return 0;
+            }
+            found = mr == MATCH_FOUND;
+            if (!found) legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
+        }
+        if (!found) break;                                      // :195-196
         z = mask | VALID.andnot(tb_nonzero<CF>(P));            // :199 + TB==0 cells
         z = fire_specials<CF, 6>(P, z);
         reward += score<CF, 6>(P, z);
@@ -880,27 +874,37 @@ M3_HD void init_board(typename CF::Bd* P, RNG& mt) {
 template <class CF>
 struct TileGen {
     static constexpr int TWMAX = 21;  // 624 tiles at most, + funnel pad
+    static constexpr int MAXR = 624 / CF::N + 2;  // rounds one MT block can feed
 };
 
+// wave-wide "any": the stream below is generated in wave-uniform chunks
+M3_HD bool wave_any(bool p) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __any((int)p) != 0;
+#else
+    return p;
+#endif
+}
+
 template <class CF, class RNG, class RawSink, class AccSink, class S = NoStore>
-M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, int stride, uint32_t& draws, uint32_t rawn,
-                            RawSink raw_sink, AccSink acc_sink, S* ps = nullptr) {
+M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* pos, int stride, uint32_t& draws,
+                            uint32_t rawn, RawSink raw_sink, AccSink acc_sink, S* ps = nullptr) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
-    constexpr int TW = TileGen<CF>::TWMAX, N = CF::N;
+    constexpr int TW = TileGen<CF>::TWMAX, N = CF::N, MAXR = TileGen<CF>::MAXR;
     constexpr Bd VALID = G::valid();
     static_assert(CF::TILE_RNG > 0u, "randint(1, 2) consumes no draws");
     uint32_t cur[CF::BITS];
 #pragma unroll
     for (int p = 0; p < CF::BITS; ++p) cur[p] = 0u;
     uint32_t nt = 0u, accw = 0u;
-    // append tiles until `target` exist (or, with raw_only, until rawn raw draws)
-    auto gen = [&](uint32_t target, bool raw_only) {
-        for (;;) {
-            const uint32_t k = g.k;
-            if (raw_only ? k >= rawn : nt >= target) break;
+    // Every lane draws raw outputs [g.k, kend): the trip count is the same on
+    // all lanes (one draw per trip), so the MT19937 chain runs without
+    // divergence; tiles are appended to the lane's own stream. pos[r] records
+    // the raw position after tile r*N - 1 (what __init__ has consumed after r rounds).
+    auto gen_to = [&](uint32_t kend) {
+        for (uint32_t k = g.k; k < kend; ++k) {
             const uint32_t v = g.next32();
-            if (g.overflow) break;
             const uint32_t t = v & CF::TILE_MASK;
             const bool ok = t <= CF::TILE_RNG;
             if (k < rawn) {
@@ -923,12 +927,21 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, int stride
                         cur[p] = 0u;
                     }
                 }
+                if (nt % (uint32_t)N == 0u && nt / (uint32_t)N < (uint32_t)MAXR) pos[(nt / N) * stride] = k + 1u;
             }
         }
-        if ((nt >> 5) < (uint32_t)TW) {  // the partial word, so the round can read it
+        if ((nt >> 5) < (uint32_t)TW) {  // the partial word, so a round can read it
 #pragma unroll
             for (int p = 0; p < CF::BITS; ++p) tm[(p * TW + (int)(nt >> 5)) * stride] = cur[p];
         }
+    };
+    // make sure every lane that still needs them has `need` tiles (or the block is exhausted)
+    auto ensure = [&](uint32_t need, bool want) {
+        while (wave_any(want && nt < need) && g.k < 624u) {
+            const uint32_t kend = g.k + 64u < 624u ? g.k + 64u : 624u;
+            gen_to(kend);
+        }
+        return !want || nt >= need;
     };
     auto take = [&](uint32_t j, Bd* T) {  // tiles [j, j + N) as planes
         const int q = (int)(j >> 5);
@@ -948,30 +961,35 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, int stride
     if constexpr (HasProf<S>::value) ps->template mark<PH_LOAD>();
 #pragma unroll
     for (int p = 0; p < CF::NP; ++p) P[p] = Bd::zero();
-    gen((uint32_t)N, false);                                   // :21
-    if (g.overflow) return false;
-    take(0u, P);
+    bool ok = ensure((uint32_t)N, true);                       // :21
+    if (ok) take(0u, P);
     if constexpr (HasProf<S>::value) ps->template mark<PH_REFILL>();
-    uint32_t j = (uint32_t)N;
+    uint32_t rounds = 1u;
+    bool live = ok;
     Bd mask;
     for (;;) {                                                 // :23-27
-        const bool any = get_match_mask<CF>(P, mask);
+        const bool any = live && get_match_mask<CF>(P, mask);
         if constexpr (HasProf<S>::value) ps->template mark<PH_MATCH>();
-        if (!any) break;
-        gen(j + (uint32_t)N, false);
-        if (g.overflow || j + (uint32_t)N > (uint32_t)(32 * TW)) return false;
-        Bd T[CF::BITS];
-        take(j, T);
+        live = any;
+        const uint32_t need = (rounds + 1u) * (uint32_t)N;
+        const bool have = ensure(need, live);
+        if (live && !have) ok = false;
+        live = live && have;
+        if (!wave_any(live)) break;
+        if (live) {
+            Bd T[CF::BITS];
+            take(rounds * (uint32_t)N, T);
 #pragma unroll
-        for (int p = 0; p < CF::BITS; ++p) P[p] = P[p].andnot(mask) | (T[p] & mask);
-        j += (uint32_t)N;
+            for (int p = 0; p < CF::BITS; ++p) P[p] = P[p].andnot(mask) | (T[p] & mask);
+            ++rounds;
+        }
         if constexpr (HasProf<S>::value) ps->template mark<PH_REFILL>();
     }
-    draws = g.k;
-    gen(0u, true);  // complete the step's stream cache: raw draws [0, rawn)
+    draws = ok ? pos[rounds * stride] : 0u;
+    if (g.k < rawn) gen_to(rawn);  // complete the step's stream cache: raw draws [0, rawn)
     if (rawn & 31u) acc_sink(rawn >> 5, accw);
     if constexpr (HasProf<S>::value) ps->template mark<PH_NEXT>();
-    return true;
+    return ok;
 }
 
 // --------------------------------------------------------------------------

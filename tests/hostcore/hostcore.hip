@@ -61,17 +61,18 @@ template <class CF>
 static int step_cached(typename CF::Bd* P, const int8_t* board, uint32_t seed, int na, int act, uint32_t& f,
                        int32_t& draws, uint32_t* legal, int32_t& next_act, int& recomputed) {
     using SC = StreamCache<CF>;
-    typename SC::RawT raw[SC::RAWN], raw2[SC::RAWN];
+    alignas(16) typename SC::RawT raw[SC::RAWN];
+    typename SC::RawT raw2[SC::RAWN];
     uint32_t ts[CF::BITS * (SC::TSW + 1)], acc[SC::ACCW], ts2[CF::BITS * (SC::TSW + 1)], acc2[SC::ACCW];
     // the cache as reset builds it (init_board_tiles) ...
     {
-        static uint32_t tm[CF::BITS * TileGen<CF>::TWMAX];
+        static uint32_t tm[CF::BITS * TileGen<CF>::TWMAX], pos[TileGen<CF>::MAXR];
         memset(tm, 0, sizeof(tm));
         typename CF::Bd Q[CF::NP];
         ChainMT g;
         g.init(seed, mt_state397(seed));
         uint32_t d;
-        init_board_tiles<CF>(Q, g, tm, 1, d, (uint32_t)SC::RAWN,
+        init_board_tiles<CF>(Q, g, tm, pos, 1, d, (uint32_t)SC::RAWN,
                              [&](uint32_t k, uint32_t v) { raw[k] = (typename SC::RawT)v; },
                              [&](uint32_t w, uint32_t v) { acc[w] = v; });
         for (int p = 0; p < CF::BITS; ++p) {
@@ -167,14 +168,15 @@ static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const in
 template <class CF>
 static int init_n(long n, const uint32_t* seeds, int8_t* out, int32_t* draws, uint32_t* m397, int32_t* first_act) {
     int recomputed = 0;
-    static uint32_t tm[CF::BITS * TileGen<CF>::TWMAX];
+    static uint32_t tm[CF::BITS * TileGen<CF>::TWMAX], pos[TileGen<CF>::MAXR];
     for (long i = 0; i < n; ++i) {
         typename CF::Bd P[CF::NP], HL, VL;
         m397[i] = mt_state397(seeds[i]);
         ChainMT cm;
         cm.init(seeds[i], m397[i]);
         uint32_t d = 0;
-        const bool ok = init_board_tiles<CF>(P, cm, tm, 1, d, 0u, [](uint32_t, uint32_t) {}, [](uint32_t, uint32_t) {});
+        const bool ok =
+            init_board_tiles<CF>(P, cm, tm, pos, 1, d, 0u, [](uint32_t, uint32_t) {}, [](uint32_t, uint32_t) {});
         draws[i] = (int32_t)d;
         if (!ok) {
             recomputed++;

@@ -16,7 +16,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "element-crush-gym_amd")
-os.environ["M3_LIB"] = os.path.join(PKG, "build", "libm3_prof.so")
+_lib = "libm3_prof.so"
+for i, a in enumerate(sys.argv):
+    if a == "--lib" and i + 1 < len(sys.argv):
+        _lib = sys.argv[i + 1]
+os.environ["M3_LIB"] = os.path.join(PKG, "build", _lib)
 sys.path.insert(0, PKG)
 
 import numpy as np  # noqa: E402
@@ -33,6 +37,7 @@ def main():
     ap.add_argument("--shards", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--shape", default="9x9x6")
+    ap.add_argument("--lib", default="libm3_prof.so", help="profiling build under element-crush-gym_amd/build")
     a = ap.parse_args()
     R, C, T = (int(x) for x in a.shape.split("x"))
     L = _native.lib()
