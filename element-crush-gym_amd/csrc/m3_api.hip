@@ -79,7 +79,8 @@ constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 template <class CF>
 struct KS {
     static constexpr int B = 64;
-    static constexpr int GCAP = CF::N > 128 ? 4 : 8;
+    static constexpr int GCAP = 4;                  // match groups in LDS (more spill to a global pool)
+    static constexpr uint32_t SPILL_RECORDS = 4096;  // spill pool records per shard
     // per-board stream cache of the batched env (m3_rules.hpp, StreamCache)
     using SC = StreamCache<CF>;
     static constexpr int RAWN = SC::RAWN, ACCW = SC::ACCW, TSW = SC::TSW;
@@ -89,11 +90,15 @@ struct KS {
     using Rng = typename SC::Rng;
 };
 
-// Per-lane match-group table in LDS (see m3_rules.hpp, match_scan). Entry
-// (g, h|v, word i) of lane l lives at tab[((g*2 + hv)*W + i)*LANES + l]:
-// consecutive lanes hit consecutive dwords, so every access is conflict-free.
+// Per-lane match-group table (see m3_rules.hpp, match_scan): the first CAP
+// groups in LDS, entry (g, h|v, word i) of lane l at tab[((g*2 + hv)*W + i)*LANES + l]
+// (consecutive lanes hit consecutive dwords: conflict-free). A board that
+// forms more groups in one scan (~1e-3 of steps at CAP 4) takes a record from
+// a small global spill pool for groups CAP..MAXG-1; only a full pool (never in
+// practice) sends the step to the exact recompute pass.
+// LDS-only table (stateless kernels: a board with more groups is recomputed by k_apply_fix)
 template <class CF, int CAP_, int LANES>
-struct LdsStore {
+struct LdsTable {
     static constexpr int CAP = CAP_;
     static constexpr int W = CF::W;
     static constexpr int BLOCK = LANES;
@@ -111,12 +116,63 @@ struct LdsStore {
         for (int i = 0; i < W; ++i) r.w[i] = tab[((g * 2 + 1) * W + i) * BLOCK];
         return r;
     }
-    __device__ __forceinline__ void put(int g, const typename CF::Bd& h, const typename CF::Bd& v) {
+    __device__ __forceinline__ bool put(int g, const typename CF::Bd& h, const typename CF::Bd& v) {
 #pragma unroll
         for (int i = 0; i < W; ++i) {
             tab[((g * 2) * W + i) * BLOCK] = h.w[i];
             tab[((g * 2 + 1) * W + i) * BLOCK] = v.w[i];
         }
+        return true;
+    }
+};
+
+template <class CF, int CAP_, int LANES>
+struct LdsStore {
+    static constexpr int CAP = CF::MAXG;     // logical capacity (spill included)
+    static constexpr int LCAP = CAP_;        // groups held in LDS
+    static constexpr int W = CF::W;
+    static constexpr int BLOCK = LANES;
+    static constexpr int WORDS = LCAP * 2 * W * BLOCK;
+    static constexpr int SPILL_WORDS = (CF::MAXG - LCAP) * 2 * W;  // per pool record
+    uint32_t* tab;        // already offset by threadIdx.x
+    uint32_t* spill;      // nullable: pool of records
+    uint32_t* pool_next;  // pool allocation counter
+    uint32_t pool_cap;
+    uint32_t rec = ~0u;   // this lane's record
+    __device__ __forceinline__ typename CF::Bd get(int g, int hv) const {
+        typename CF::Bd r;
+        if (g < LCAP) {
+#pragma unroll
+            for (int i = 0; i < W; ++i) r.w[i] = tab[((g * 2 + hv) * W + i) * BLOCK];
+        } else {
+            const uint32_t* p = spill + (size_t)rec * SPILL_WORDS + ((g - LCAP) * 2 + hv) * W;
+#pragma unroll
+            for (int i = 0; i < W; ++i) r.w[i] = p[i];
+        }
+        return r;
+    }
+    __device__ __forceinline__ typename CF::Bd get_h(int g) const { return get(g, 0); }
+    __device__ __forceinline__ typename CF::Bd get_v(int g) const { return get(g, 1); }
+    __device__ __forceinline__ bool put(int g, const typename CF::Bd& h, const typename CF::Bd& v) {
+        if (g < LCAP) {
+#pragma unroll
+            for (int i = 0; i < W; ++i) {
+                tab[((g * 2) * W + i) * BLOCK] = h.w[i];
+                tab[((g * 2 + 1) * W + i) * BLOCK] = v.w[i];
+            }
+            return true;
+        }
+        if (rec == ~0u) rec = atomicAdd(pool_next, 1u);
+        const bool ok = rec < pool_cap;
+        if (ok) {
+            uint32_t* p = spill + (size_t)rec * SPILL_WORDS + (g - LCAP) * 2 * W;
+#pragma unroll
+            for (int i = 0; i < W; ++i) {
+                p[i] = h.w[i];
+                p[W + i] = v.w[i];
+            }
+        }
+        return ok;
     }
 };
 
@@ -321,7 +377,7 @@ __global__ void __launch_bounds__(KS<CF>::B) k_apply(ApplyArgs a) {
         const uint32_t s = a.seeds[b];
         ChainMT rng;
         rng.init(s, mt_state397(s));
-        LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};
+        LdsTable<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};  // overflow -> k_apply_fix
         if (!apply_and_emit<CF>(P, a, b, rng, st)) {
             const uint32_t slot = atomicAdd(a.ovf_count, 1u);
             a.ovf_list[slot] = (uint32_t)b;
@@ -351,33 +407,70 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
     }
 }
 
+constexpr int NSLOT = 4;            // episode slots per board (see EnvArgs)
+constexpr int PF_LAG = NSLOT - 1;   // steps between a prefetch and its first use
+
+// A reset launch processes "items". Item i is (board b, seed, slot): with a
+// list (env prefetch) b = list[i], seed = list_seed[i], slot = list_slot[i];
+// without, b = i, seed = seeds[i] + seed_add, slot = slot_of ? (slot_of[b] +
+// slot0) % NSLOT : slot0. Per-board outputs go to index ob = slot * sstride + b
+// (sstride 0 = the env's current state, n = one of the episode slots).
 struct InitArgs {
     int64_t n;
-    const uint32_t* seeds;       // stateless: seeds[i]; env: seeds[b] (+stride when autoreset)
-    const uint32_t* list;        // nullable: board index list (env autoreset)
-    const uint32_t* list_count;  // nullable: device count for list
-    uint32_t stride;             // env autoreset seed increment (0 = keep seeds)
-    uint32_t* seeds_out;         // nullable: env seed table to update
-    int8_t* boards;
-    uint32_t* draws;         // nullable
-    int32_t* first_action;   // nullable
-    uint32_t* legal;         // nullable
-    uint32_t* mt397;         // nullable
-    int32_t* score;          // nullable (env)
-    int32_t* moves;          // nullable (env)
-    int32_t* reward;         // nullable (env: zeroed on explicit reset)
-    uint8_t* done;           // nullable
-    uint8_t* trunc;          // nullable
-    uint32_t* flags;         // nullable
-    uint32_t* ovf_count;     // boards whose init needed >= 624 draws (FullMT recompute)
-    uint32_t* ovf_list;
-    // nullable: env stream cache (KS<CF>): raw rows [b][RAWN], tile planes and
-    // acceptance words SoA with board stride cstride
+    const uint32_t* list;        // nullable
+    const uint32_t* list_seed;
+    const uint32_t* list_slot;
+    const uint32_t* list_count;  // device count for list
+    const uint32_t* seeds;       // implicit items
+    uint32_t seed_add;
+    uint32_t slot0;
+    const uint8_t* slot_of;      // nullable
+    int64_t sstride;
+    int8_t* boards;              // cells as bytes at ob * N            (one of boards /
+    uint32_t* board_words;       // cells as LE words at ob * NW         board_words)
+    uint32_t* draws;             // nullable
+    int32_t* first_action;       // nullable
+    uint32_t* legal;             // nullable
+    int32_t* score;              // nullable: zeroed episode state (explicit env reset)
+    int32_t* moves;
+    int32_t* reward;
+    uint8_t* done;
+    uint8_t* trunc;
+    uint32_t* flags;
+    uint32_t* ovf_count;         // items whose reset needed >= 624 draws (k_init_fix)
+    uint32_t* ovf_list;          // item indices
+    uint32_t* stats;             // nullable: [0] resets, [1] reset recomputes
+    // nullable: stream cache of slot s, board b: raw row (s*cstride + b)*RAWN,
+    // tile word (p, w) at s*TS_WORDS*cstride + (p*TSW + w)*cstride + b,
+    // acceptance word w at s*ACCW*cstride + w*cstride + b
     void* sraw;
     uint32_t* sts;
     uint32_t* sacc;
     int64_t cstride;
 };
+
+__device__ __forceinline__ void init_item(const InitArgs& a, int64_t i, int64_t& b, uint32_t& seed, uint32_t& slot) {
+    if (a.list) {
+        b = (int64_t)a.list[i];
+        seed = a.list_seed[i];
+        slot = a.list_slot[i];
+    } else {
+        b = i;
+        seed = a.seeds[b] + a.seed_add;
+        slot = a.slot_of ? ((uint32_t)a.slot_of[b] + a.slot0) % (uint32_t)NSLOT : a.slot0;
+    }
+}
+
+template <class CF>
+__device__ __forceinline__ void init_store_board(const InitArgs& a, int64_t ob, const uint32_t* cw) {
+    constexpr int NW = (CF::N + 3) / 4;
+    if (a.board_words) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) a.board_words[ob * NW + q] = cw[q];
+    } else {
+        store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.boards + ob * CF::N), cw);
+    }
+}
 
 // BoardV2.__init__ (boardv2.py:17-27) + first seeded random action
 // (samplerTasks.py:11-13) for board b. Returns false if the stream overflowed.
@@ -385,7 +478,7 @@ struct InitArgs {
 // random action (np.random.seed(cfg.seed) then choice(legal), samplerTasks.py:11-13),
 // the cached mt[397] and the zeroed episode state.
 template <class CF>
-__device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, uint32_t seed, uint32_t m397,
+__device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, int64_t ob, uint32_t seed, uint32_t m397,
                                              uint32_t draws, const typename CF::Bd* P) {
     typename CF::Bd HL, VL;
     legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
@@ -394,10 +487,9 @@ __device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, uint3
     ChainMT rng;
     rng.init(seed, m397);
     const int fa = random_action<CF>(act, rng);
-    if (a.draws) a.draws[b] = draws;
-    if (a.first_action) a.first_action[b] = fa;
-    if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
-    if (a.mt397) a.mt397[b] = m397;
+    if (a.draws) a.draws[ob] = draws;
+    if (a.first_action) a.first_action[ob] = fa;
+    if (a.legal) store_legal<CF>(a.legal + ob * CF::AW, act);
     if (a.score) a.score[b] = 0;
     if (a.moves) a.moves[b] = 0;
     if (a.reward) a.reward[b] = 0;
@@ -410,15 +502,18 @@ __device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, uint3
 // the env's cache pointers set it also writes the step's stream cache.
 // Returns false if the reset needs >= 624 draws (k_init_fix redoes it).
 template <class CF, class S = NoStore>
-__device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t m397, uint32_t* tm,
-                                          uint32_t* pos, S* ps = nullptr) {
+__device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t slot, uint32_t m397,
+                                          uint32_t* tm, uint32_t* pos, S* ps = nullptr) {
     using K = KS<CF>;
     using RawT = typename K::RawT;
     constexpr int TW = TileGen<CF>::TWMAX;
     typename CF::Bd P[CF::NP];
     ChainMT g;
     g.init(seed, m397);
-    RawT* row = a.sraw ? static_cast<RawT*>(a.sraw) + b * K::RAWN : nullptr;
+    const int64_t cb = (int64_t)slot * a.cstride + b;  // cache row of (slot, b)
+    RawT* row = a.sraw ? static_cast<RawT*>(a.sraw) + cb * K::RAWN : nullptr;
+    uint32_t* sacc = a.sacc ? a.sacc + (int64_t)slot * K::ACCW * a.cstride + b : nullptr;
+    uint32_t* sts = a.sts ? a.sts + (int64_t)slot * K::TS_WORDS * a.cstride + b : nullptr;
     uint32_t draws = 0;
     constexpr uint32_t PER = 4u / sizeof(RawT), SH = 8u * sizeof(RawT);
     uint32_t pk = 0u;  // PER raw entries per dword store (k is the same on every lane)
@@ -431,19 +526,20 @@ __device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t
                 pk = 0u;
             }
         },
-        [&](uint32_t w, uint32_t v) { a.sacc[(int64_t)w * a.cstride + b] = v; }, ps);
-    if (a.sts) {
+        [&](uint32_t w, uint32_t v) { sacc[(int64_t)w * a.cstride] = v; }, ps);
+    if (sts) {
 #pragma unroll
         for (int p = 0; p < CF::BITS; ++p)
 #pragma unroll
-            for (int w = 0; w < K::TSW; ++w) a.sts[(int64_t)(p * K::TSW + w) * a.cstride + b] = tm[(p * TW + w) * INIT_BLOCK];
+            for (int w = 0; w < K::TSW; ++w) sts[(int64_t)(p * K::TSW + w) * a.cstride] = tm[(p * TW + w) * INIT_BLOCK];
     }
     if (!ok) return false;
-    init_outputs<CF>(a, b, seed, m397, draws, P);
+    const int64_t ob = (int64_t)slot * a.sstride + b;
+    init_outputs<CF>(a, b, ob, seed, m397, draws, P);
     constexpr int NW = (CF::N + 3) / 4;
     uint32_t cw[NW];
     words_from_planes<CF>(P, cw);
-    store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.boards + b * CF::N), cw);
+    init_store_board<CF>(a, ob, cw);
     return true;
 }
 
@@ -451,7 +547,7 @@ __device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t
 template <class CF>
 __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
-    if (a.list_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.ovf_count + 8, (uint32_t)cnt);  // stats: resets
+    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.stats[0], (uint32_t)cnt);
     __shared__ uint32_t tm_s[CF::BITS * TileGen<CF>::TWMAX * INIT_BLOCK];
     __shared__ uint32_t pos_s[TileGen<CF>::MAXR * INIT_BLOCK];
     uint32_t* tm = tm_s + threadIdx.x;
@@ -467,18 +563,18 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
 #endif
     for (int64_t i = (int64_t)blockIdx.x * INIT_BLOCK + threadIdx.x; i < cnt;
          i += (int64_t)gridDim.x * INIT_BLOCK) {
-        const int64_t b = a.list ? (int64_t)a.list[i] : i;
-        const uint32_t seed = a.seeds[b] + a.stride;
-        if (a.seeds_out) a.seeds_out[b] = seed;
+        int64_t b;
+        uint32_t seed, slot;
+        init_item(a, i, b, seed, slot);
         const uint32_t m397 = mt_state397(seed);
 #ifdef M3_PHASE_PROF
-        const bool ok = init_emit<CF>(a, b, seed, m397, tm, pos, &ps);
+        const bool ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, &ps);
 #else
-        const bool ok = init_emit<CF>(a, b, seed, m397, tm, pos, pp);
+        const bool ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, pp);
 #endif
         if (!ok) {
-            const uint32_t slot = atomicAdd(a.ovf_count, 1u);
-            a.ovf_list[slot] = (uint32_t)b;
+            const uint32_t o = atomicAdd(a.ovf_count, 1u);
+            a.ovf_list[o] = (uint32_t)i;
         }
     }
 #ifdef M3_PHASE_PROF
@@ -574,10 +670,11 @@ __global__ void __launch_bounds__(64 * WC_WAVES) k_init_fix(InitArgs a) {
     uint32_t* key = key_s[wv];
     uint8_t* cells = cell_s[wv];
     const uint32_t cnt = *a.ovf_count;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(a.ovf_count + 7, cnt);  // stats: reset recomputes
-    for (uint32_t i = blockIdx.x * WC_WAVES + wv; i < cnt; i += gridDim.x * WC_WAVES) {
-        const int64_t b = a.ovf_list[i];
-        const uint32_t seed = a.seeds_out ? a.seeds_out[b] : a.seeds[b] + a.stride;
+    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[1], cnt);
+    for (uint32_t oi = blockIdx.x * WC_WAVES + wv; oi < cnt; oi += gridDim.x * WC_WAVES) {
+        int64_t b;
+        uint32_t seed, slot;
+        init_item(a, (int64_t)a.ovf_list[oi], b, seed, slot);
         if (lane == 0) {  // init_genrand is a serial recurrence
             uint32_t x = seed;
             for (uint32_t p = 0; p < 624u; ++p) {
@@ -595,9 +692,15 @@ __global__ void __launch_bounds__(64 * WC_WAVES) k_init_fix(InitArgs a) {
             wave_fill<CF>(key, cells, lane, pos, k, &mask);
             planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
         }
-        if (lane == 0) init_outputs<CF>(a, b, seed, m397, k, P);
-        int8_t* dst = a.boards + b * CF::N;
-        for (int x = lane; x < CF::N; x += 64) dst[x] = (int8_t)cells[x];
+        const int64_t ob = (int64_t)slot * a.sstride + b;
+        if (lane == 0) init_outputs<CF>(a, b, ob, seed, m397, k, P);
+        if (a.board_words) {
+            for (int q = lane; q < (CF::N + 3) / 4; q += 64)
+                a.board_words[ob * ((CF::N + 3) / 4) + q] = reinterpret_cast<const uint32_t*>(cells)[q];
+        } else {
+            int8_t* dst = a.boards + ob * CF::N;
+            for (int x = lane; x < CF::N; x += 64) dst[x] = (int8_t)cells[x];
+        }
         wave_sync();
     }
 }
@@ -623,15 +726,23 @@ __global__ void __launch_bounds__(KS<CF>::B) k_legal(int64_t n, const int8_t* bo
 // ---------------------------------------------------------------------------
 // batched env (n x Match3Env, env.py:8-65)
 // ---------------------------------------------------------------------------
+// Autoreset keeps NSLOT episode slots per board: the current episode's stream
+// cache is slot cur[b]; slots cur+1 .. cur+NSLOT-1 hold the next episodes
+// (seed + k*stride) -- initial board, first action, legal set and stream
+// cache -- computed ahead by the prefetch pass (k_init on its own stream). A
+// finished board swaps in slot cur+1 inside the step and queues slot cur (now
+// free) for the episode NSLOT-1 ahead; the prefetch of step t is only needed
+// NSLOT-1 steps later, so resets never sit on the step's critical path.
+
 struct EnvArgs {
     int64_t n;
     int num_moves, goal;
     int autoreset;
+    uint32_t stride;         // autoreset seed increment
     const int8_t* cur;
     int8_t* nxt;
     const int32_t* actions;  // nullable -> next_action
     uint32_t* seeds;
-    uint32_t* mt397;
     int32_t* score;
     int32_t* moves;
     int32_t* next_action;
@@ -642,16 +753,26 @@ struct EnvArgs {
     uint32_t* draws;
     uint32_t* legal;  // nullable
     int32_t* packed;  // nullable: reward<<2 | trunc<<1 | done for the RCCL gather
-    uint32_t* counters;  // [0] overflow count, [1] reset count
+    uint32_t* counters;  // this step's block: [0] overflow count, [1] prefetch count, [3] spill records used
+    uint32_t* spill;     // group-table spill pool of the shard
+    uint32_t* stats;     // [0] step recomputes
     uint32_t* ovf_list;
-    uint32_t* reset_list;
-    const void* sraw;    // stream cache (see InitArgs)
+    uint8_t* slot;       // current episode slot per board
+    const uint32_t* ne_words;  // episode slots: initial cells (LE words) [3][n][NW]
+    const int32_t* ne_first;   // [3][n] first seeded random action
+    const uint32_t* ne_legal;  // [3][n][AW]
+    uint32_t* pf_list;   // prefetch queue of this step: board, seed, slot
+    uint32_t* pf_seed;
+    uint32_t* pf_slot;
+    const void* sraw;    // stream caches of the 3 slots (layout: InitArgs)
     const uint32_t* sts;
     const uint32_t* sacc;
     int64_t cstride;
 };
 
-// Match3Env.step bookkeeping (env.py:48-56) around BoardV2.apply_action.
+// Match3Env.step bookkeeping (env.py:48-56) around BoardV2.apply_action, and
+// the same-step autoreset (the finished step's reward/done/flags stay visible,
+// the observation and episode state become the next episode's).
 template <class CF, class RNG, class Store>
 __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st) {
     // every per-board input is loaded before the cascade, so its latency hides behind it
@@ -677,23 +798,48 @@ __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& 
         if (na < 0) f |= FLAG_NO_LEGAL;
     }
     mark<PH_NEXT>(st);
-    a.score[b] = sc;
-    a.moves[b] = mv1;
     a.reward[b] = r;
     a.trunc[b] = (uint8_t)tr;
     a.done[b] = (uint8_t)dn;
     a.flags[b] = f;
-    a.next_action[b] = na;
-    if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
     if (a.packed) a.packed[b] = (r << 2) | (tr << 1) | dn;
-    if (a.autoreset) {  // append to the reset list: one atomic per wave, not per lane
-        const uint64_t m = __ballot(dn);
-        if (m) {
-            const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&a.counters[1], (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            if (dn) a.reset_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)b;
+    const bool reset = dn && a.autoreset;
+    if (!reset) {
+        a.score[b] = sc;
+        a.moves[b] = mv1;
+        a.next_action[b] = na;
+        if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
+    } else {  // swap in the prefetched next episode (slot + 1)
+        constexpr int NW = (CF::N + 3) / 4;
+        const uint32_t s_old = a.slot[b], s_new = s_old + 1u == (uint32_t)NSLOT ? 0u : s_old + 1u;
+        const int64_t ob = (int64_t)s_new * a.cstride + b;  // slots are strided by the env's n
+        const uint32_t seed = a.seeds[b] + a.stride;
+        uint32_t cw[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) cw[q] = a.ne_words[ob * NW + q];
+        planes_from_words<CF>(cw, P);
+        a.slot[b] = (uint8_t)s_new;
+        a.seeds[b] = seed;
+        a.score[b] = 0;
+        a.moves[b] = 0;
+        a.next_action[b] = a.ne_first[ob];
+        if (a.legal) {
+#pragma unroll
+            for (int i = 0; i < CF::AW; ++i) a.legal[b * CF::AW + i] = a.ne_legal[ob * CF::AW + i];
+        }
+    }
+    // queue the freed slot for the episode after next: one atomic per wave, not per lane
+    const uint64_t m = __ballot(reset);
+    if (m) {
+        const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&a.counters[1], (uint32_t)__popcll(m));
+        base = __shfl(base, leader);
+        if (reset) {
+            const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            a.pf_list[q] = (uint32_t)b;
+            a.pf_seed[q] = a.seeds[b] + (uint32_t)(NSLOT - 1) * a.stride;
+            a.pf_slot[q] = a.slot[b] == 0u ? (uint32_t)(NSLOT - 1) : a.slot[b] - 1u;
         }
     }
     return true;
@@ -709,18 +855,22 @@ __global__ void __launch_bounds__(KS<CF>::B) k_env_step(EnvArgs a) {
     const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
     block_copy_in<CF::N, KS<CF>::B>(a.cur + b0 * CF::N, lds, nb);
     const int t = threadIdx.x;
+    uint32_t cslot = 0u;
     if (t < nb) {  // this lane's tile planes (+ zero pad) and acceptance words, lane-interleaved
         const int64_t b = b0 + t;
+        cslot = a.slot[b];
+        const uint32_t* sts = a.sts + (int64_t)cslot * K::TS_WORDS * a.cstride + b;
+        const uint32_t* sacc = a.sacc + (int64_t)cslot * K::ACCW * a.cstride + b;
 #pragma unroll
         for (int p = 0; p < CF::BITS; ++p) {
 #pragma unroll
             for (int w = 0; w < K::TSW; ++w)
-                cache_s[(p * (K::TSW + 1) + w) * K::B + t] = a.sts[(int64_t)(p * K::TSW + w) * a.cstride + b];
+                cache_s[(p * (K::TSW + 1) + w) * K::B + t] = sts[(int64_t)(p * K::TSW + w) * a.cstride];
             cache_s[(p * (K::TSW + 1) + K::TSW) * K::B + t] = 0u;
         }
 #pragma unroll
         for (int w = 0; w < K::ACCW; ++w)
-            cache_s[(CF::BITS * (K::TSW + 1) + w) * K::B + t] = a.sacc[(int64_t)w * a.cstride + b];
+            cache_s[(CF::BITS * (K::TSW + 1) + w) * K::B + t] = sacc[(int64_t)w * a.cstride];
     }
     __syncthreads();
 #ifdef M3_PHASE_PROF
@@ -733,13 +883,16 @@ __global__ void __launch_bounds__(KS<CF>::B) k_env_step(EnvArgs a) {
 #else
     LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};
 #endif
+    st.spill = a.spill;
+    st.pool_next = &a.counters[3];
+    st.pool_cap = K::SPILL_RECORDS;
     if (t < nb) {
         const int64_t b = b0 + t;
         typename CF::Bd P[CF::NP];
         lds_to_planes<CF>(lds, t, P);
         typename K::Rng rng;
-        rng.init(static_cast<const typename K::RawT*>(a.sraw) + b * K::RAWN, cache_s + t,
-                 cache_s + CF::BITS * (K::TSW + 1) * K::B + t, K::B);
+        rng.init(static_cast<const typename K::RawT*>(a.sraw) + ((int64_t)cslot * a.cstride + b) * K::RAWN,
+                 cache_s + t, cache_s + CF::BITS * (K::TSW + 1) * K::B + t, K::B);
         if (!env_step_one<CF>(P, a, b, rng, st)) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
             a.ovf_list[slot] = (uint32_t)b;
@@ -756,7 +909,7 @@ __global__ void __launch_bounds__(KS<CF>::B) k_env_step(EnvArgs a) {
 template <class CF>
 __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
     const uint32_t cnt = a.counters[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.counters[8], cnt);  // stats: step recomputes
+    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], cnt);
     for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
@@ -765,9 +918,7 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
         mt.init(a.seeds[b], 0u);
         ArrayStore<CF> st;
         env_step_one<CF>(P, a, b, mt, st);
-        uint8_t tmp[CF::N];
-        planes_to_bytes<CF>(P, tmp);
-        for (int x = 0; x < CF::N; ++x) a.nxt[b * CF::N + x] = (int8_t)tmp[x];
+        planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * CF::N));
     }
 }
 
@@ -813,15 +964,27 @@ struct m3_env {
     bool ready = false;
     int8_t* boards[2] = {nullptr, nullptr};
     int cur = 0;
-    uint32_t *seeds = nullptr, *mt397 = nullptr, *flags = nullptr, *draws = nullptr, *legal = nullptr;
+    uint32_t *seeds = nullptr, *flags = nullptr, *draws = nullptr, *legal = nullptr;
     int32_t *score = nullptr, *moves = nullptr, *next_action = nullptr, *reward = nullptr;
     uint8_t *done = nullptr, *trunc = nullptr;
     int32_t* actions = nullptr;
+    // counters, 64 words per shard: [4q + 0] step overflow count, [4q + 1]
+    // prefetch queue length, [4q + 2] prefetch overflow count (q = step % PF_LAG);
+    // stats [16] step recomputes, [17] resets, [18] reset recomputes
     uint32_t* counters = nullptr;
-    uint32_t *ovf_list = nullptr, *reset_list = nullptr, *init_ovf_list = nullptr;
-    // per-board stream cache (KS<CF>): raw rows, tile planes, acceptance words
+    uint32_t* ovf_list = nullptr;
+    uint32_t* spill = nullptr;  // group-table spill pools, one per shard slot
+    // NSLOT episode slots per board (see EnvArgs): the current episode's
+    // stream cache + the next episodes' initial state and cache
+    uint8_t* slot = nullptr;
+    uint32_t* ne_words = nullptr;
+    int32_t* ne_first = nullptr;
+    uint32_t* ne_legal = nullptr;
     void* sraw = nullptr;
     uint32_t *sts = nullptr, *sacc = nullptr;
+    // prefetch queues and their overflow lists, by step % PF_LAG
+    uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {}, *pf_ovf[PF_LAG] = {};
+    int64_t steps = 0;
     int32_t* packed = nullptr;
     int32_t* gathered = nullptr;
     ncclComm_t comm = nullptr;
@@ -830,13 +993,15 @@ struct m3_env {
     // the i-th k_env_step launch since m3_env_timing(enable)
     std::vector<hipEvent_t> tev;
     int tcap = 0, tn = 0;
-    // Independent board shards, one HIP stream each. A shard's step ->
-    // fixup -> reset chain is serial, but the reset of a finished shard is a
-    // small latency-bound launch that overlaps the other shards' step kernels.
+    // Independent board shards, each with a step stream (step + fixup) and a
+    // prefetch stream (next-episode resets). Step t of a shard waits only for
+    // the prefetch of step t - PF_LAG, so resets overlap the following steps.
     struct Shard {
         int64_t off = 0, n = 0;
-        hipStream_t stream = nullptr;
-        hipEvent_t ev = nullptr;
+        hipStream_t stream = nullptr, pstream = nullptr;
+        hipEvent_t ev = nullptr;       // last step work of this shard
+        hipEvent_t pev[PF_LAG] = {};   // prefetch of queue q done
+        bool ppending[PF_LAG] = {};
     };
     std::vector<Shard> shards;
     hipEvent_t gather_ev = nullptr;
@@ -913,25 +1078,45 @@ int launch_legal(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* legal) {
 // autoreset k_init + k_init_fix over the boards that finished. Every pointer
 // is offset to the shard, so kernels see shard-local board indices.
 template <class CF>
+void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
+    r.sstride = e->n;
+    r.board_words = e->ne_words + o * ((CF::N + 3) / 4);
+    r.first_action = e->ne_first + o;
+    r.legal = e->ne_legal + o * CF::AW;
+    r.sraw = static_cast<typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
+    r.sts = e->sts + o;
+    r.sacc = e->sacc + o;
+    r.cstride = e->n;
+}
+
+// Enqueue one env step of shard s: on the step stream, wait for the prefetch
+// of two steps ago, zero this parity's counters, k_env_step (cur -> nxt, with
+// the in-step autoreset swap) and k_env_fix (exact recompute of overflowed
+// boards); on the prefetch stream, k_init + k_init_fix over the queued slots.
+// Every pointer is offset to the shard, so kernels see shard-local indices.
+template <class CF>
 int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     m3_ctx* c = e->ctx;
-    const m3_env::Shard& sh = e->shards[s];
+    m3_env::Shard& sh = e->shards[s];
     if (sh.n == 0) return M3_OK;
     const int64_t o = sh.off;
     const int N = c->N, AW = c->AW;
-    uint32_t* cnt = e->counters + 64 * s;
+    const int par = (int)(e->steps % PF_LAG);
+    uint32_t* base = e->counters + 64 * s;
+    uint32_t* cnt = base + 4 * par;
     hipStream_t st = sh.stream;
     if (e->gather_pending) HIP_TRY(hipStreamWaitEvent(st, e->gather_ev, 0));  // `packed` still being read
+    if (sh.ppending[par]) HIP_TRY(hipStreamWaitEvent(st, sh.pev[par], 0));  // queue + slots of step t - PF_LAG
     EnvArgs a;
     a.n = sh.n;
     a.num_moves = e->num_moves;
     a.goal = e->goal;
     a.autoreset = e->autoreset;
+    a.stride = e->stride;
     a.cur = e->boards[e->cur] + o * N;
     a.nxt = e->boards[e->cur ^ 1] + o * N;
     a.actions = d_actions ? d_actions + o : nullptr;
     a.seeds = e->seeds + o;
-    a.mt397 = e->mt397 + o;
     a.score = e->score + o;
     a.moves = e->moves + o;
     a.next_action = e->next_action + o;
@@ -943,8 +1128,16 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.legal = e->legal + o * AW;
     a.packed = e->packed + o;
     a.counters = cnt;
+    a.spill = e->spill + (size_t)s * KS<CF>::SPILL_RECORDS * LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::SPILL_WORDS;
+    a.stats = base + 16;
     a.ovf_list = e->ovf_list + o;
-    a.reset_list = e->reset_list + o;
+    a.slot = e->slot + o;
+    a.ne_words = e->ne_words + o * ((N + 3) / 4);
+    a.ne_first = e->ne_first + o;
+    a.ne_legal = e->ne_legal + o * AW;
+    a.pf_list = e->pf_list[par] + o;
+    a.pf_seed = e->pf_seed[par] + o;
+    a.pf_slot = e->pf_slot[par] + o;
     a.sraw = static_cast<const typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
     a.sts = e->sts + o;
     a.sacc = e->sacc + o;
@@ -960,32 +1153,25 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     }
     hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(sh.ev, st));
     if (e->autoreset) {
+        HIP_TRY(hipStreamWaitEvent(sh.pstream, sh.ev, 0));
         InitArgs r{};
         r.n = sh.n;
-        r.seeds = e->seeds + o;
-        r.list = e->reset_list + o;
+        r.list = e->pf_list[par] + o;
+        r.list_seed = e->pf_seed[par] + o;
+        r.list_slot = e->pf_slot[par] + o;
         r.list_count = &cnt[1];
-        r.stride = e->stride;
-        r.seeds_out = e->seeds + o;
-        r.boards = e->boards[e->cur ^ 1] + o * N;
-        r.first_action = e->next_action + o;
-        r.legal = e->legal + o * AW;
-        r.mt397 = e->mt397 + o;
-        r.score = e->score + o;
-        r.moves = e->moves + o;
         r.ovf_count = &cnt[2];
-        r.ovf_list = e->init_ovf_list + o;
-        r.sraw = static_cast<typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
-        r.sts = e->sts + o;
-        r.sacc = e->sacc + o;
-        r.cstride = e->n;
-        // reward/done/trunc/flags of the finished step stay visible; the grid
-        // is sized for the expected number of finished boards and grid-strides
-        int rc = launch_init<CF>(st, r, sh.n / 8 + 1);
+        r.ovf_list = e->pf_ovf[par] + o;
+        r.stats = base + 17;
+        prefetch_args<CF>(e, o, r);
+        // the grid is sized for the expected number of finished boards and grid-strides
+        int rc = launch_init<CF>(sh.pstream, r, sh.n / 8 + 1);
         if (rc) return rc;
+        HIP_TRY(hipEventRecord(sh.pev[par], sh.pstream));
+        sh.ppending[par] = true;
     }
-    HIP_TRY(hipEventRecord(sh.ev, st));
     return M3_OK;
 }
 
@@ -997,6 +1183,7 @@ int launch_env_step(m3_env* e, const int32_t* d_actions) {
     }
     e->gather_pending = false;
     e->cur ^= 1;
+    e->steps++;
     return M3_OK;
 }
 
@@ -1008,8 +1195,45 @@ int join_shards(m3_env* e, hipStream_t st) {
 }
 
 int sync_env(m3_env* e) {
-    for (auto& sh : e->shards) HIP_TRY(hipStreamSynchronize(sh.stream));
+    for (auto& sh : e->shards) {
+        HIP_TRY(hipStreamSynchronize(sh.stream));
+        HIP_TRY(hipStreamSynchronize(sh.pstream));
+        for (bool& p : sh.ppending) p = false;
+    }
     HIP_TRY(hipStreamSynchronize(e->ctx->stream));
+    return M3_OK;
+}
+
+void destroy_shards(m3_env* e) {
+    for (auto& sh : e->shards) {
+        (void)hipStreamDestroy(sh.stream);
+        (void)hipStreamDestroy(sh.pstream);
+        (void)hipEventDestroy(sh.ev);
+        for (hipEvent_t ev : sh.pev) (void)hipEventDestroy(ev);
+    }
+    e->shards.clear();
+}
+
+// Episode slots cur + 1 .. cur + NSLOT - 1 of every board from its current
+// seed (explicit reset, or autoreset switched on later).
+template <class CF>
+int fill_next_slots(m3_env* e) {
+    m3_ctx* c = e->ctx;
+    for (uint32_t k = 1; k < (uint32_t)NSLOT; ++k) {
+        InitArgs r{};
+        r.n = e->n;
+        r.seeds = e->seeds;
+        r.seed_add = k * e->stride;
+        r.slot0 = k;
+        r.slot_of = e->slot;
+        r.ovf_count = &e->counters[32 + k];
+        r.ovf_list = e->pf_ovf[0];
+        prefetch_args<CF>(e, 0, r);
+        HIP_TRY(hipMemsetAsync(r.ovf_count, 0, 4, c->stream));
+        int rc = launch_init<CF>(c->stream, r, e->n);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return M3_OK;
 }
 
@@ -1229,7 +1453,6 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     alloc(&e->boards[0], bytes);
     alloc(&e->boards[1], bytes);
     alloc(&e->seeds, n * 4);
-    alloc(&e->mt397, n * 4);
     alloc(&e->flags, n * 4);
     alloc(&e->draws, n * 4);
     alloc(&e->legal, n * 4ull * c->AW);
@@ -1242,14 +1465,24 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     alloc(&e->actions, n * 4);
     alloc(&e->counters, 64 * 4 * MAX_SHARDS);
     alloc(&e->ovf_list, n * 4);
-    alloc(&e->reset_list, n * 4);
-    alloc(&e->init_ovf_list, n * 4);
     alloc(&e->packed, n * 4);
+    alloc(&e->slot, n);
+    alloc(&e->ne_words, (size_t)NSLOT * n * 4ull * ((c->N + 3) / 4));
+    alloc(&e->ne_first, (size_t)NSLOT * n * 4);
+    alloc(&e->ne_legal, (size_t)NSLOT * n * 4ull * c->AW);
+    for (int p = 0; p < PF_LAG; ++p) {
+        alloc(&e->pf_list[p], n * 4);
+        alloc(&e->pf_seed[p], n * 4);
+        alloc(&e->pf_slot[p], n * 4);
+        alloc(&e->pf_ovf[p], n * 4);
+    }
     with_shape(c->shape, [&](auto cf) {
         using K = KS<decltype(cf)>;
-        alloc(&e->sraw, n * (size_t)K::RAWN * sizeof(typename K::RawT));
-        alloc(&e->sts, n * 4ull * K::TS_WORDS);
-        alloc(&e->sacc, n * 4ull * K::ACCW);
+        using St = LdsStore<decltype(cf), K::GCAP, K::B>;
+        alloc(&e->spill, (size_t)MAX_SHARDS * K::SPILL_RECORDS * St::SPILL_WORDS * 4);
+        alloc(&e->sraw, (size_t)NSLOT * n * (size_t)K::RAWN * sizeof(typename K::RawT));
+        alloc(&e->sts, (size_t)NSLOT * n * 4ull * K::TS_WORDS);
+        alloc(&e->sacc, (size_t)NSLOT * n * 4ull * K::ACCW);
         return 0;
     });
     if (err == hipSuccess) err = hipEventCreateWithFlags(&e->gather_ev, hipEventDisableTiming);
@@ -1272,19 +1505,17 @@ int m3_env_set_shards(m3_env* e, int nshards) {
     HIP_TRY(hipSetDevice(e->ctx->device));
     int rc = sync_env(e);
     if (rc) return rc;
-    for (auto& sh : e->shards) {
-        (void)hipStreamDestroy(sh.stream);
-        (void)hipEventDestroy(sh.ev);
-    }
-    e->shards.clear();
-    // shard boundaries on 256-board workgroup multiples
+    destroy_shards(e);
+    // shard boundaries on 256-board multiples
     const int64_t per = ((e->n + nshards - 1) / nshards + BLOCK - 1) / BLOCK * BLOCK;
     for (int s = 0; s < nshards; ++s) {
         m3_env::Shard sh;
         sh.off = std::min<int64_t>(e->n, s * per);
         sh.n = std::min<int64_t>(e->n, sh.off + per) - sh.off;
         HIP_TRY(hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&sh.pstream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&sh.ev, hipEventDisableTiming));
+        for (hipEvent_t& ev : sh.pev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         e->shards.push_back(sh);
     }
     return M3_OK;
@@ -1300,17 +1531,17 @@ int m3_env_destroy(m3_env* e) {
     if (!e) return M3_OK;
     (void)hipSetDevice(e->ctx->device);
     (void)sync_env(e);
-    for (auto& sh : e->shards) {
-        (void)hipStreamDestroy(sh.stream);
-        (void)hipEventDestroy(sh.ev);
-    }
+    destroy_shards(e);
     if (e->gather_ev) (void)hipEventDestroy(e->gather_ev);
-    void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->mt397, e->flags, e->draws, e->legal,
-                    e->score, e->moves, e->next_action, e->reward, e->done, e->trunc, e->actions,
-                    e->counters, e->ovf_list, e->reset_list, e->init_ovf_list, e->packed, e->gathered,
-                    e->sraw, e->sts, e->sacc};
+    void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->flags, e->draws, e->legal, e->score, e->moves,
+                    e->next_action, e->reward, e->done, e->trunc, e->actions, e->counters, e->ovf_list,
+                    e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal, e->sraw, e->sts,
+                    e->sacc, e->spill};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    for (int q = 0; q < PF_LAG; ++q)
+        for (void* p : {(void*)e->pf_list[q], (void*)e->pf_seed[q], (void*)e->pf_slot[q], (void*)e->pf_ovf[q]})
+            if (p) (void)hipFree(p);
     if (e->comm) ncclCommDestroy(e->comm);
     for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
     delete e;
@@ -1340,7 +1571,6 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     a.boards = e->boards[e->cur];
     a.first_action = e->next_action;
     a.legal = e->legal;
-    a.mt397 = e->mt397;
     a.score = e->score;
     a.moves = e->moves;
     a.reward = e->reward;
@@ -1348,14 +1578,20 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     a.trunc = e->trunc;
     a.flags = e->flags;
     a.draws = e->draws;
-    a.ovf_count = &e->counters[2];
-    a.ovf_list = e->init_ovf_list;
-    a.sraw = e->sraw;
+    a.ovf_count = &e->counters[32];
+    a.ovf_list = e->pf_ovf[0];
+    a.sraw = e->sraw;  // episode slot 0
     a.sts = e->sts;
     a.sacc = e->sacc;
     a.cstride = e->n;
     HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));  // also clears the stats
-    int rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, e->n); });
+    HIP_TRY(hipMemsetAsync(e->slot, 0, e->n, c->stream));
+    e->steps = 0;
+    int rc = with_shape(c->shape, [&](auto cf) {
+        int r = launch_init<decltype(cf)>(c->stream, a, e->n);
+        if (r == M3_OK && e->autoreset) r = fill_next_slots<decltype(cf)>(e);
+        return r;
+    });
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     e->ready = true;
@@ -1364,8 +1600,14 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
 
 int m3_env_set_autoreset(m3_env* e, int enabled, uint32_t seed_stride) {
     CHECK_ARG(e, "null env");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    int rc = sync_env(e);
+    if (rc) return rc;
+    const bool refill = enabled && e->ready && (!e->autoreset || e->stride != seed_stride);
     e->autoreset = enabled ? 1 : 0;
     e->stride = seed_stride;
+    if (refill)  // the queued next episodes depend on the stride
+        return with_shape(e->ctx->shape, [&](auto cf) { return fill_next_slots<decltype(cf)>(e); });
     return M3_OK;
 }
 
@@ -1479,9 +1721,9 @@ int m3_env_stats(m3_env* e, uint64_t out[4]) {
     HIP_TRY(hipMemcpy(h.data(), e->counters, h.size() * 4, hipMemcpyDeviceToHost));
     out[0] = out[1] = out[2] = out[3] = 0;
     for (size_t s = 0; s < e->shards.size(); ++s) {
-        out[0] += h[64 * s + 8];   // steps recomputed (>= 624 draws or > table groups)
-        out[1] += h[64 * s + 9];   // resets recomputed by the wave-cooperative pass (>= 624 draws)
-        out[2] += h[64 * s + 10];  // autoresets
+        out[0] += h[64 * s + 16];  // steps recomputed (cache exhausted or > table groups)
+        out[1] += h[64 * s + 18];  // resets recomputed by the wave-cooperative pass (>= 624 draws)
+        out[2] += h[64 * s + 17];  // autoresets (episodes prefetched)
     }
     out[3] = e->shards.size();
     return M3_OK;

@@ -287,9 +287,10 @@ struct ArrayStore {
     typename CF::Bd v[CAP];
     M3_HD typename CF::Bd get_h(int g) const { return h[g]; }
     M3_HD typename CF::Bd get_v(int g) const { return v[g]; }
-    M3_HD void put(int g, const typename CF::Bd& hh, const typename CF::Bd& vv) {
+    M3_HD bool put(int g, const typename CF::Bd& hh, const typename CF::Bd& vv) {
         h[g] = hh;
         v[g] = vv;
+        return true;
     }
 };
 
@@ -301,9 +302,10 @@ struct SmallStore {
     typename CF::Bd v[CAP];
     M3_HD typename CF::Bd get_h(int g) const { return h[g]; }
     M3_HD typename CF::Bd get_v(int g) const { return v[g]; }
-    M3_HD void put(int g, const typename CF::Bd& hh, const typename CF::Bd& vv) {
+    M3_HD bool put(int g, const typename CF::Bd& hh, const typename CF::Bd& vv) {
         h[g] = hh;
         v[g] = vv;
+        return true;
     }
 };
 
@@ -391,10 +393,10 @@ M3_HD int match_scan(const typename CF::Bd* P, typename CF::Bd& mask, typename C
                 }
             }
             if (g < 0) {
-                if (ng == Store::CAP) return MATCH_OVERFLOW;
-                st.put(ng++, rh, rv);
-            } else {
-                st.put(g, st.get_h(g) | rh, st.get_v(g) | rv);
+                if (ng == Store::CAP || !st.put(ng, rh, rv)) return MATCH_OVERFLOW;
+                ++ng;
+            } else if (!st.put(g, st.get_h(g) | rh, st.get_v(g) | rv)) {
+                return MATCH_OVERFLOW;
             }
             vruns |= rv;
         }

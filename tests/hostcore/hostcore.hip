@@ -137,6 +137,16 @@ static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const in
             SmallStore<CF, 8> ss;
             rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
                                   next_act[i], recomputed);
+        } else if (small == 5 || small == 6) {  // candidate device table sizes
+            if (small == 5) {
+                SmallStore<CF, 5> ss;
+                rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
+                                      next_act[i], recomputed);
+            } else {
+                SmallStore<CF, 6> ss;
+                rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
+                                      next_act[i], recomputed);
+            }
         } else if (small == 4 || small == 2) {  // candidate smaller device tables
             if (small == 4) {
                 SmallStore<CF, 4> ss;
