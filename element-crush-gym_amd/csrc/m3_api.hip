@@ -66,7 +66,8 @@ int set_err(int code, const char* fmt, ...) {
 
 constexpr int BLOCK = 256;
 constexpr int FIX_BLOCK = 64;
-constexpr int FIX_GRID = 256;
+constexpr int FIX_GRID = 16;       // step fixup almost never has work: few blocks schedule fast
+constexpr int INIT_FIX_GRID = 64;  // ~1% of resets: one board per wave
 constexpr int INIT_BLOCK = 64;
 constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 
@@ -1060,7 +1061,7 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_init_fix<CF>, dim3(FIX_GRID), dim3(64 * WC_WAVES), 0, stream, a);
+    hipLaunchKernelGGL(k_init_fix<CF>, dim3(INIT_FIX_GRID), dim3(64 * WC_WAVES), 0, stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }

@@ -88,9 +88,9 @@ struct Cfg {
 // stream per plane, ACCW words of acceptance bitmap.
 template <class CF>
 struct StreamCache {
-    static constexpr int RAWN = CF::N > 128 ? 512 : 256;
+    static constexpr int RAWN = CF::N > 128 ? 512 : 320;
     static constexpr int ACCW = RAWN / 32;
-    static constexpr int TSW = CF::N > 128 ? 8 : 4;
+    static constexpr int TSW = CF::N > 128 ? 8 : 5;
     using RawT = std::conditional_t<(CF::A > 256), uint16_t, uint8_t>;
     using Rng = CachedRNG<RawT, RAWN, CF::BITS, TSW, ACCW>;
 };
