@@ -80,6 +80,9 @@ def main():
     ap.add_argument("--goal", type=int, default=500)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shards", type=int, default=None, help="board shards (HIP streams) per GPU; default: library's")
+    ap.add_argument("--no-autoreset", action="store_true",
+                    help="diagnostic only: boards stop at done (later steps are terminal no-ops); not the headline")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -99,7 +102,8 @@ def main():
 
     B = args.boards
     env = BatchedMatch3Env(B, rows, cols, types, num_moves=args.moves, env_goal=args.goal, device=local,
-                           seed_base=1 + rank * B, autoreset=True, seed_stride=world * B)
+                           seed_base=1 + rank * B, autoreset=not args.no_autoreset, seed_stride=world * B,
+                           shards=args.shards)
     if world > 1:
         obj = [env.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -140,7 +144,9 @@ def main():
     total_steps = world * B * args.steps
     value = total_steps / elapsed
     avg_kernel_s = float(kms.mean()) / 1e3 if len(kms) else float("nan")
-    bytes_per_launch = B * algorithmic_bytes_per_step(rows, cols)
+    # one k_env_step launch processes one shard (B / shards boards, contiguous, the last may be short)
+    shard_boards = -(-B // stats["shards"])
+    bytes_per_launch = shard_boards * algorithmic_bytes_per_step(rows, cols)
     achieved = bytes_per_launch / avg_kernel_s / 1e9
     traffic = load_traffic(args.shape, B)
     out = {
@@ -166,6 +172,7 @@ def main():
             "env_goal": args.goal,
             "parallelism": f"dp{world}",
             "shards_per_gpu": stats["shards"],
+            "autoreset": not args.no_autoreset,
         },
         "path_stats": {"autoresets": stats["autoresets"], "reset_recomputes": stats["reset_recomputes"],
                        "step_recomputes": stats["step_recomputes"]},
@@ -178,6 +185,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "algorithmic_bytes_per_launch": bytes_per_launch,
+            "boards_per_launch": shard_boards,
             "avg_kernel_ms": avg_kernel_s * 1e3,
             "note": "integer-VALU bound path; HBM roofline per BASELINE/SURVEY §8(d): 183 B per 9x9 env-step",
         },

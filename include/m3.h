@@ -97,9 +97,9 @@ int m3_env_destroy(m3_env *env);
 int m3_env_reset(m3_env *env, const uint32_t *seeds, uint32_t seed_base);
 
 /* Split the boards into nshards (1..8) contiguous shards, each stepped on its
- * own HIP stream; a shard's small, latency-bound autoreset launch then
- * overlaps the other shards' step kernels. Results do not depend on it.
- * Default: one shard per 262,144 boards, at most 4. */
+ * own HIP stream (plus one prefetch stream per shard for the autoreset
+ * launches). Results do not depend on it. Default: 1 (fastest measured: the
+ * prefetch stream already overlaps resets with the single step launch). */
 int m3_env_set_shards(m3_env *env, int nshards);
 /* Wait for all work of the env (every shard stream). */
 int m3_env_synchronize(m3_env *env);

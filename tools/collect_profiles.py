@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Copy a gpu_round.sh run's evidence into profiles/ (tracked) and derive profiles/traffic.json.
+
+    python3 tools/collect_profiles.py gpurun_out/<tag> <round-tag>
+
+Writes profiles/<round-tag>_bench.json (the bench line), <round-tag>_kernel_stats.csv
+(rocprofv3 --kernel-trace --stats of the same bench command), <round-tag>_pmc.txt
+(per-kernel PMC means, one rocprofv3 pass per counter group) and traffic.json:
+HBM bytes per k_env_step launch = 2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes), the
+factor 2 being MI355X_MICROARCH.md's gfx950 correction for wide coalesced reads
+(FETCH_SIZE reports half of them; narrower accesses are uncalibrated).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+src, tag = sys.argv[1], sys.argv[2]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = os.path.join(ROOT, "profiles")
+
+
+def last_json(path):
+    return json.loads(open(path).read().strip().splitlines()[-1])
+
+
+bench = last_json(os.path.join(src, "bench.log"))
+json.dump(bench, open(os.path.join(P, f"{tag}_bench.json"), "w"), indent=1)
+shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(P, f"{tag}_kernel_stats.csv"))
+pmc = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), src],
+                     capture_output=True, text=True, check=True).stdout
+open(os.path.join(P, f"{tag}_pmc.txt"), "w").write(pmc)
+
+agg = collections.defaultdict(list)
+for f in glob.glob(f"{src}/**/*_counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "k_env_step" in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+fetch = sum(agg["FETCH_SIZE"]) / len(agg["FETCH_SIZE"]) * 1024
+write = sum(agg["WRITE_SIZE"]) / len(agg["WRITE_SIZE"]) * 1024
+cfg = bench["config"]
+traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"], "kernel": "k_env_step",
+           "boards_per_launch": bench["roofline"].get("boards_per_launch"),
+           "fetch_size_bytes": fetch, "write_size_bytes": write,
+           "hbm_bytes_per_launch": 2 * fetch + write,
+           "bytes_per_board": (2 * fetch + write) / bench["roofline"].get("boards_per_launch", cfg["boards_per_gpu"]),
+           "source": f"profiles/{tag}_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
+           "correction": "2 x FETCH_SIZE (gfx950 wide-read calibration) + WRITE_SIZE"}
+json.dump(traffic, open(os.path.join(P, "traffic.json"), "w"), indent=1)
+print(json.dumps(traffic, indent=1))
