@@ -93,6 +93,7 @@ def main():
     if not os.path.exists(os.path.join(PKG, "build", "libm3.so")):
         subprocess.run(["make", "-C", PKG], check=True)
     from match3tile.batched import BatchedMatch3Env
+    from match3tile.distributed import seed_plan, timed_steps
 
     dist = None
     if world > 1:
@@ -101,8 +102,9 @@ def main():
         dist.init_process_group("gloo")
 
     B = args.boards
+    seed_base, seed_stride = seed_plan(rank, world, B)
     env = BatchedMatch3Env(B, rows, cols, types, num_moves=args.moves, env_goal=args.goal, device=local,
-                           seed_base=1 + rank * B, autoreset=not args.no_autoreset, seed_stride=world * B,
+                           seed_base=seed_base, autoreset=not args.no_autoreset, seed_stride=seed_stride,
                            shards=args.shards)
     if world > 1:
         obj = [env.comm_unique_id() if rank == 0 else None]
@@ -114,24 +116,8 @@ def main():
         if world > 1:
             env.gather()
 
-    for _ in range(args.warmup):
-        step()
-    env.synchronize()
-    if dist:
-        dist.barrier()
-    env.enable_timing(args.steps)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    env.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        dist.barrier()
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_steps(step, env.synchronize, args.steps, args.warmup, dist,
+                          on_start=lambda: env.enable_timing(args.steps))
     kms = env.kernel_ms()
     stats = env.stats()
     env.close()

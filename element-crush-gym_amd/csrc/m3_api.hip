@@ -81,6 +81,11 @@ template <class CF>
 struct KS {
     static constexpr int B = 64;
     static constexpr int GCAP = 4;                  // match groups in LDS (more spill to a global pool)
+#ifndef M3_STEP_WPS
+#define M3_STEP_WPS 3
+#endif
+    // k_env_step waves per SIMD the register allocation is bounded for
+    static constexpr int STEP_WPS = CF::N > 128 ? 1 : M3_STEP_WPS;
     static constexpr uint32_t SPILL_RECORDS = 4096;  // spill pool records per shard
     // per-board stream cache of the batched env (m3_rules.hpp, StreamCache)
     using SC = StreamCache<CF>;
@@ -847,10 +852,18 @@ __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& 
 }
 
 template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B) k_env_step(EnvArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[KS<CF>::B * CF::N + 16];
-    __shared__ uint32_t gtab[LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::WORDS];
+__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArgs a) {
+    // The board staging area is only live before the cascade (HBM -> LDS ->
+    // planes) and after it (planes -> LDS -> HBM), the match-group table only
+    // inside it; with one wave per workgroup nothing else can touch the LDS
+    // in between, so the two share storage (13.3 KB per wave at 9x9: 3 waves/SIMD).
     using K = KS<CF>;
+    static_assert(K::B == 64, "staging/table aliasing assumes one wave per workgroup");
+    constexpr int STAGE_WORDS = (K::B * CF::N + 16 + 3) / 4;
+    constexpr int TAB_WORDS = LdsStore<CF, K::GCAP, K::B>::WORDS;
+    __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
+    uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
+    uint32_t* const gtab = stage_tab;
     __shared__ uint32_t cache_s[K::LDS_WORDS * K::B];
     const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
     const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
