@@ -69,6 +69,70 @@ def load_traffic(shape_tag, boards):
     return None
 
 
+def bench_rollouts(a):
+    """--rollouts: device MCTS rollouts (m3_rollouts_device), one launch per timed step.
+
+    n = --boards states (fresh seeded boards, n_actions = --moves, distinct cfg
+    and rollout seeds) resident in HBM before timing (torch only allocates the
+    device buffers); prints rollouts/s and the env-steps/s inside them, and the
+    C oracle's rate on a bounded host sample (which also checks the gains)."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from match3tile import _native
+
+    R, C, T = (int(x) for x in a.shape.split("x"))
+    ctx = _native.Context(R, C, T)
+    n = a.boards
+    seeds = np.arange(1, n + 1, dtype=np.uint32)
+    boards = np.empty((n, R * C), np.int8)
+    chunk = 1 << 18
+    for i in range(0, n, chunk):
+        boards[i:i + chunk] = ctx.init_boards(seeds[i:i + chunk])[0].reshape(-1, R * C)
+    rseeds = (np.arange(n, dtype=np.uint64) * 2654435761 % (2**31)).astype(np.uint32)
+    dev = torch.device("cuda", 0)
+    d_boards = torch.from_numpy(boards).to(dev)
+    d_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    d_na = torch.full((n,), a.moves, dtype=torch.int32, device=dev)
+    d_rs = torch.from_numpy(rseeds.view(np.int32)).to(dev)
+    outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
+    torch.cuda.synchronize()
+    L = _native.lib()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def run():
+        _native.check(L.m3_rollouts_device(ctx.handle, n, p(d_boards), p(d_seeds), p(d_na), p(d_rs),
+                                           *[p(o) for o in outs], None))
+
+    for _ in range(max(1, a.warmup)):
+        run()
+    _native.check(L.m3_ctx_synchronize(ctx.handle))
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        run()
+    _native.check(L.m3_ctx_synchronize(ctx.handle))
+    dt = (time.perf_counter() - t0) / a.steps
+    steps = int(outs[1].sum().item())
+    res = {"metric": "MCTS rollouts/s (device, m3_rollouts_device)", "shape": a.shape, "rollouts": n,
+           "moves": a.moves, "ms_per_launch": dt * 1e3, "rollouts_per_s": n / dt, "env_steps_per_s": steps / dt,
+           "steps_per_rollout": steps / n}
+    if not a.no_cpu_baseline:
+        from oracle import Oracle
+
+        o = Oracle(R, C, T)
+        m = min(n, 20000)
+        threads = min(16, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        r = o.rollouts(boards[:m].astype(np.int32), seeds[:m], a.moves, rseeds[:m], threads=threads)
+        cdt = time.perf_counter() - t0
+        assert (r["gain"] == outs[0][:m].cpu().numpy()).all(), "device rollouts differ from the oracle"
+        res["cpu_baseline"] = {"rollouts_per_s": m / cdt, "env_steps_per_s": float(r["steps"].sum()) / cdt,
+                               "cores": threads, "kind": "port", "sample": f"{m} rollouts, oracle/m3_oracle.c"}
+    print(json.dumps(res))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -83,7 +147,11 @@ def main():
     ap.add_argument("--shards", type=int, default=None, help="board shards (HIP streams) per GPU; default: library's")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="diagnostic only: boards stop at done (later steps are terminal no-ops); not the headline")
+    ap.add_argument("--rollouts", action="store_true",
+                    help="secondary bench: device MCTS rollouts (f3) instead of the env step")
     args = ap.parse_args()
+    if args.rollouts:
+        return bench_rollouts(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,7 +218,7 @@ def main():
         "data": "synthetic: seeded initial boards (seed = 1 + board index), seeded random_action per move "
                 "(samplerTasks.random_task contract), 20-move episodes, autoreset with seed += n_boards",
         "config": {
-            "workload": f"C3: {B:,} boards per GPU, {rows}x{cols}x{types}, Match3Env.step x {args.steps} "
+            "workload": f"{'C3' if (rows, cols) == (9, 9) else 'C4'}: {B:,} boards per GPU, {rows}x{cols}x{types}, Match3Env.step x {args.steps} "
                         "(step kernel + overflow fixup + autoreset; RCCL reward/done all-gather when N>1)",
             "boards_per_gpu": B,
             "shape": args.shape,

@@ -937,6 +937,136 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// batched MCTS rollouts (mctslib/standard/mcts.py:14-19)
+// ---------------------------------------------------------------------------
+// One rollout per lane: np.random.seed(rseed); while n_actions >= 1:
+// action = choice(legal_actions) from the global stream, state =
+// apply_action(action). The first choice reads the stream of rseed; every
+// later one reads the stream apply_action left behind (cfg.seed reseeded at
+// boardv2.py:46, advanced by the step's draws), i.e. the same register chain
+// the step just used. The match-group table is the env's LDS table + spill
+// pool, and a lane keeps its spill record for the whole rollout; a rollout
+// that overflows the chain (>= 624 draws in one step) or the pool is
+// replayed from its first move by k_rollout_fix.
+struct RolloutArgs {
+    int64_t n;
+    const int8_t* boards;
+    const uint32_t* seeds;     // cfg.seed of each state
+    const int32_t* n_actions;
+    const uint32_t* rseeds;    // rollout seed (random.randint(0, 2**31 - 1) or state.seed)
+    int32_t* gain;             // sum of the step rewards of the rollout
+    int32_t* steps;            // apply_action calls
+    uint32_t* draws;           // global-stream draws since its last seed when the rollout ends
+    uint32_t* flags;           // OR of the steps' M3_FLAG_*
+    int8_t* out_boards;        // nullable: terminal boards
+    uint32_t* counters;        // [0] overflow count, [1] spill records taken
+    uint32_t* ovf_list;
+    uint32_t* spill;
+    uint32_t spill_cap;
+};
+
+template <class CF, class RNG, class Store>
+__device__ __forceinline__ bool rollout_one(typename CF::Bd* P, const RolloutArgs& a, int64_t b, RNG& first, RNG& rng,
+                                            Store& st) {
+    int n = a.n_actions[b];
+    int gain = 0, steps = 0;
+    uint32_t fl = 0u, dr = 0u;
+    if (n >= 1) {                                               // mcts.py:16 while not is_terminal
+        typename CF::Bd HL, VL;
+        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
+        uint32_t act[CF::AW];
+        action_bits<CF>(HL, VL, act);
+        int x = random_action<CF>(act, first);                  // mcts.py:17, stream of the rollout seed
+        dr = first.draws();
+        for (;;) {
+            if (x < 0) {                                        // np.random.choice([]) raises
+                fl |= FLAG_NO_LEGAL;
+                break;
+            }
+            uint32_t f;
+            const int r = apply_action<CF>(P, n, x, rng, f, HL, VL, st);  // mcts.py:18
+            if (f & FLAG_RECOMPUTE) return false;
+            fl |= f;
+            gain += r;
+            ++steps;
+            --n;
+            dr = rng.draws();
+            if (n < 1) break;
+            action_bits<CF>(HL, VL, act);
+            x = random_action<CF>(act, rng);                    // stream where apply_action left it
+            if (rng.overflow) return false;
+            dr = rng.draws();
+        }
+    }
+    a.gain[b] = gain;
+    a.steps[b] = steps;
+    a.draws[b] = dr;
+    a.flags[b] = fl;
+    return true;
+}
+
+template <class CF>
+__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_rollout(RolloutArgs a) {
+    using K = KS<CF>;
+    static_assert(K::B == 64, "staging/table aliasing assumes one wave per workgroup");
+    // staging and match-group table share the LDS (as in k_env_step)
+    constexpr int STAGE_WORDS = (K::B * CF::N + 16 + 3) / 4;
+    constexpr int TAB_WORDS = LdsStore<CF, K::GCAP, K::B>::WORDS;
+    __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
+    uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
+    const int64_t b0 = (int64_t)blockIdx.x * K::B;
+    const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
+    block_copy_in<CF::N, K::B>(a.boards + b0 * CF::N, lds, nb);
+    __syncthreads();
+    const int t = threadIdx.x;
+    typename CF::Bd P[CF::NP];
+    if (t < nb) lds_to_planes<CF>(lds, t, P);
+    __syncthreads();
+    LdsStore<CF, K::GCAP, K::B> st{stage_tab + t};
+    st.spill = a.spill;
+    st.pool_next = &a.counters[1];
+    st.pool_cap = a.spill_cap;
+    if (t < nb) {
+        const int64_t b = b0 + t;
+        const uint32_t rs = a.rseeds[b], s = a.seeds[b];
+        ChainMT first, rng;
+        first.init(rs, mt_state397(rs));
+        rng.init(s, mt_state397(s));
+        if (!rollout_one<CF>(P, a, b, first, rng, st)) {
+            const uint32_t o = atomicAdd(&a.counters[0], 1u);
+            a.ovf_list[o] = (uint32_t)b;
+        }
+    }
+    if (!a.out_boards) return;
+    __syncthreads();
+    if (t < nb) planes_to_bytes<CF>(P, lds + t * CF::N);
+    __syncthreads();
+    block_copy_out<CF::N, K::B>(a.out_boards + b0 * CF::N, lds, nb);
+}
+
+// exact replay of overflowed rollouts: 624-word MT19937 states and the full
+// group table in lane-private scratch
+template <class CF>
+__global__ void __launch_bounds__(FIX_BLOCK) k_rollout_fix(RolloutArgs a) {
+    const uint32_t cnt = a.counters[0];
+    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
+        const int64_t b = a.ovf_list[i];
+        typename CF::Bd P[CF::NP];
+        bytes_to_planes<CF>(a.boards + b * CF::N, P);
+        FullMT first, rng;
+        first.init(a.rseeds[b], 0u);
+        rng.init(a.seeds[b], 0u);
+        ArrayStore<CF> st;
+        rollout_one<CF>(P, a, b, first, rng, st);
+        if (a.out_boards) {
+            uint8_t tmp[CF::N];
+            planes_to_bytes<CF>(P, tmp);
+            for (int x = 0; x < CF::N; ++x) a.out_boards[b * CF::N + x] = (int8_t)tmp[x];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // shape dispatch
 // ---------------------------------------------------------------------------
 #define M3_SHAPES(X) \
@@ -1026,6 +1156,7 @@ namespace {
 
 int ensure_scratch(m3_ctx* c, size_t bytes) {
     if (c->dcap >= bytes) return M3_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));  // async work may still use the old buffer
     if (c->dbuf) HIP_TRY(hipFree(c->dbuf));
     c->dbuf = nullptr;
     c->dcap = 0;
@@ -1444,6 +1575,118 @@ int m3_legal_actions(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* out_l
     rc = with_shape(c->shape, [&](auto cf) { return launch_legal<decltype(cf)>(c, n, d_in, d_out); });
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(out_legal_bits, d_out, n * 4ull * c->AW, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return M3_OK;
+}
+
+// ---- rollouts ---------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+// overflow list + group-table spill pool of a rollout launch (a lane keeps one
+// spill record for its whole rollout)
+int64_t rollout_spill_cap(int64_t n) { return std::max<int64_t>(4096, n / 8); }
+
+size_t rollout_spill_words(int shape) {
+    return (size_t)with_shape(shape, [&](auto cf) {
+        using CF = decltype(cf);
+        return (int)LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::SPILL_WORDS;
+    });
+}
+
+// a.n and the per-rollout buffers set; carves the pool from cv and launches
+int enqueue_rollouts(m3_ctx* c, RolloutArgs a, Carve& cv) {
+    const int64_t cap = rollout_spill_cap(a.n);
+    a.counters = c->counters;
+    a.ovf_list = cv.take<uint32_t>(a.n);
+    a.spill = cv.take<uint32_t>(cap * rollout_spill_words(c->shape));
+    a.spill_cap = (uint32_t)cap;
+    HIP_TRY(hipMemsetAsync(c->counters, 0, 16, c->stream));
+    return with_shape(c->shape, [&](auto cf) {
+        using CF = decltype(cf);
+        hipLaunchKernelGGL(k_rollout<CF>, dim3(grid_for<CF>(a.n)), dim3(KS<CF>::B), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_rollout_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+        return M3_OK;
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int m3_rollouts_device(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seeds, const int32_t* n_actions,
+                       const uint32_t* rollout_seeds, int32_t* out_gain, int32_t* out_steps, uint32_t* out_draws,
+                       uint32_t* out_flags, int8_t* out_boards) {
+    CHECK_ARG(c && n >= 0, "bad arguments");
+    if (n == 0) return M3_OK;
+    CHECK_ARG(n < (int64_t)1 << 31, "n too large");
+    CHECK_ARG(boards && seeds && n_actions && rollout_seeds && out_gain && out_steps && out_draws && out_flags,
+              "null buffer");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = ensure_scratch(c, carve_size({n * 4ull, rollout_spill_cap(n) * rollout_spill_words(c->shape) * 4ull}));
+    if (rc) return rc;
+    Carve cv{(char*)c->dbuf};
+    RolloutArgs a{};
+    a.n = n;
+    a.boards = boards;
+    a.seeds = seeds;
+    a.n_actions = n_actions;
+    a.rseeds = rollout_seeds;
+    a.gain = out_gain;
+    a.steps = out_steps;
+    a.draws = out_draws;
+    a.flags = out_flags;
+    a.out_boards = out_boards;
+    return enqueue_rollouts(c, a, cv);
+}
+
+int m3_rollouts(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seeds, const int32_t* n_actions,
+                const uint32_t* rollout_seeds, int32_t* out_gain, int32_t* out_steps, uint32_t* out_draws,
+                uint32_t* out_flags, int8_t* out_boards) {
+    CHECK_ARG(c && n >= 0, "bad arguments");
+    if (n == 0) return M3_OK;
+    CHECK_ARG(n < (int64_t)1 << 31, "n too large");
+    CHECK_ARG(boards && seeds && n_actions && rollout_seeds && out_gain && out_steps && out_draws && out_flags,
+              "null buffer");
+    for (int64_t i = 0; i < n * c->N; ++i)
+        if (boards[i] < 0) return set_err(M3_ERR_INVALID, "cell value outside [0, 127] at byte %lld", (long long)i);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = n * (size_t)c->N;
+    const size_t need = carve_size({bytes, n * 4ull, n * 4ull, n * 4ull, n * 4ull, n * 4ull, n * 4ull, n * 4ull,
+                                    out_boards ? bytes : 0, n * 4ull,
+                                    rollout_spill_cap(n) * rollout_spill_words(c->shape) * 4ull});
+    int rc = ensure_scratch(c, need);
+    if (rc) return rc;
+    Carve cv{(char*)c->dbuf};
+    RolloutArgs a{};
+    a.n = n;
+    int8_t* d_in = cv.take<int8_t>(bytes);
+    uint32_t* d_seeds = cv.take<uint32_t>(n);
+    int32_t* d_na = cv.take<int32_t>(n);
+    uint32_t* d_rs = cv.take<uint32_t>(n);
+    a.boards = d_in;
+    a.seeds = d_seeds;
+    a.n_actions = d_na;
+    a.rseeds = d_rs;
+    a.gain = cv.take<int32_t>(n);
+    a.steps = cv.take<int32_t>(n);
+    a.draws = cv.take<uint32_t>(n);
+    a.flags = cv.take<uint32_t>(n);
+    a.out_boards = out_boards ? cv.take<int8_t>(bytes) : nullptr;
+    HIP_TRY(hipMemcpyAsync(d_in, boards, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_seeds, seeds, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_na, n_actions, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_rs, rollout_seeds, n * 4, hipMemcpyHostToDevice, c->stream));
+    rc = enqueue_rollouts(c, a, cv);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out_gain, a.gain, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_steps, a.steps, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_draws, a.draws, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_flags, a.flags, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (out_boards) HIP_TRY(hipMemcpyAsync(out_boards, a.out_boards, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return M3_OK;
 }

@@ -32,7 +32,7 @@ ENV_BOARDS, ENV_REWARD, ENV_DONE, ENV_TRUNCATED, ENV_SCORE, ENV_MOVES, ENV_FLAGS
 EXPORTS = [
     "m3_abi_version", "m3_last_error", "m3_device_count", "m3_supported", "m3_action_space",
     "m3_ctx_create", "m3_ctx_destroy", "m3_ctx_synchronize",
-    "m3_init_boards", "m3_apply_actions", "m3_legal_actions",
+    "m3_init_boards", "m3_apply_actions", "m3_legal_actions", "m3_rollouts", "m3_rollouts_device",
     "m3_env_create", "m3_env_destroy", "m3_env_reset", "m3_env_set_shards", "m3_env_synchronize",
     "m3_env_set_autoreset", "m3_env_step",
     "m3_env_step_device", "m3_env_get", "m3_env_device_ptr",
@@ -76,6 +76,8 @@ def lib():
             "m3_init_boards": ([vp, i64, vp, vp, vp, vp], i32),
             "m3_apply_actions": ([vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
             "m3_legal_actions": ([vp, i64, vp, vp], i32),
+            "m3_rollouts": ([vp, i64] + [vp] * 9, i32),
+            "m3_rollouts_device": ([vp, i64] + [vp] * 9, i32),
             "m3_env_create": ([vp, i64, i32, i32, vp], i32),
             "m3_env_destroy": ([vp], i32),
             "m3_env_reset": ([vp, vp, u32], i32),
@@ -189,6 +191,29 @@ class Context:
         with self._lock:
             check(lib().m3_legal_actions(self.handle, len(b), ptr(b), ptr(out)))
         return out
+
+    def rollouts(self, boards, seeds, n_actions, rollout_seeds, final_boards=False):
+        """MCTS.rollout (mctslib/standard/mcts.py:14-19) of n states in one launch.
+
+        Returns gain (summed step rewards), steps, draws (global stream position
+        since its last seed) and flags per rollout, and optionally the terminal boards."""
+        b = self._boards(boards)
+        n = len(b)
+        seeds = np.ascontiguousarray(np.broadcast_to(np.asarray(seeds, dtype=np.uint32), (n,)))
+        na = np.ascontiguousarray(np.broadcast_to(np.asarray(n_actions, dtype=np.int32), (n,)))
+        rs = np.ascontiguousarray(np.broadcast_to(np.asarray(rollout_seeds, dtype=np.uint32), (n,)))
+        gain = np.empty(n, np.int32)
+        steps = np.empty(n, np.int32)
+        draws = np.empty(n, np.uint32)
+        flags = np.empty(n, np.uint32)
+        fin = np.empty_like(b) if final_boards else None
+        with self._lock:
+            check(lib().m3_rollouts(self.handle, n, ptr(b), ptr(seeds), ptr(na), ptr(rs), ptr(gain), ptr(steps),
+                                    ptr(draws), ptr(flags), ptr(fin)))
+        res = dict(gain=gain, steps=steps, draws=draws, flags=flags)
+        if final_boards:
+            res["final"] = fin.reshape(n, self.rows, self.columns)
+        return res
 
     def legal_actions(self, board):
         """Ascending legal action ids of one board (boardFunctions.legal_actions)."""

@@ -86,6 +86,28 @@ int m3_apply_actions(m3_ctx *ctx, int64_t n, const int8_t *boards, const uint32_
 /* legal_actions(cfg, board) (boardFunctions.py:26-112) as bitsets. */
 int m3_legal_actions(m3_ctx *ctx, int64_t n, const int8_t *boards, uint32_t *out_legal_bits);
 
+/* ---- batched MCTS rollouts (mctslib/standard/mcts.py:14-19) ------------- */
+
+/* MCTS.rollout(state) for n independent states (board, cfg.seed, n_actions):
+ * np.random.seed(rollout_seeds[i]); while n_actions >= 1: action =
+ * np.random.choice(legal_actions); state = state.apply_action(action).
+ * The first choice reads rollout_seeds[i]'s stream, later ones the stream
+ * apply_action left (cfg.seed + draws), exactly as the reference's global RNG.
+ * out_gain = sum of the step rewards (rollout return = state.reward + gain),
+ * out_steps = apply_action calls, out_draws = raw draws of the global stream
+ * since its last seed at the end (seed = cfg.seed if out_steps > 0, else
+ * rollout_seeds[i]), out_flags = OR of the steps' M3_FLAG_* (M3_FLAG_NO_LEGAL:
+ * the reference raises in np.random.choice; the rollout stops there).
+ * out_boards (nullable) = terminal boards. Host buffers; blocks until done. */
+int m3_rollouts(m3_ctx *ctx, int64_t n, const int8_t *boards, const uint32_t *seeds,
+                const int32_t *n_actions, const uint32_t *rollout_seeds, int32_t *out_gain,
+                int32_t *out_steps, uint32_t *out_draws, uint32_t *out_flags, int8_t *out_boards);
+/* Same on device buffers, enqueued on the context stream (no sync). Inputs
+ * must stay valid until the stream reaches the launch. */
+int m3_rollouts_device(m3_ctx *ctx, int64_t n, const int8_t *boards, const uint32_t *seeds,
+                       const int32_t *n_actions, const uint32_t *rollout_seeds, int32_t *out_gain,
+                       int32_t *out_steps, uint32_t *out_draws, uint32_t *out_flags, int8_t *out_boards);
+
 /* ---- device-resident batched env: n x Match3Env (env.py:8-65) ----------- */
 
 /* num_moves / env_goal as Match3Env(num_moves=20, env_goal=500) (env.py:15-16). */

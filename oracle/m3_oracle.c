@@ -575,6 +575,55 @@ void m3o_batch_episodes(const m3o_cfg *cfg, int64_t n, const uint32_t *seeds, in
     }
 }
 
+/* mctslib/standard/mcts.py:14-19. The global RNG is seeded once with the
+ * rollout seed (:15); apply_action reseeds it with cfg.seed every step
+ * (boardv2.py:46), so every choice after the first reads cfg.seed's stream
+ * where the step left it. A terminal state (n_actions < 1) returns at once. */
+int64_t m3o_rollout(const m3o_cfg *cfg, const int32_t *board, uint32_t seed, int n_actions,
+                    uint32_t rollout_seed, int32_t *final_board, int *steps, int64_t *draws, int *flags) {
+    const int N = cfg->R * cfg->C;
+    m3o_mt mt;
+    int32_t *a = (int32_t *)malloc(sizeof(int32_t) * (size_t)N);
+    int32_t *b = (int32_t *)malloc(sizeof(int32_t) * (size_t)N);
+    int32_t *legal = (int32_t *)malloc(sizeof(int32_t) * (size_t)cfg->A);
+    memcpy(a, board, sizeof(int32_t) * (size_t)N);
+    m3o_mt_seed(&mt, rollout_seed);                                         /* mcts.py:15 */
+    int64_t gain = 0;
+    *steps = 0;
+    *flags = 0;
+    while (n_actions >= 1) {                                                /* mcts.py:16 */
+        int nl = m3o_legal_actions(cfg, a, legal);
+        if (nl == 0) { *flags |= M3O_FLAG_NO_LEGAL; break; }               /* choice([]) raises */
+        int act = legal[m3o_randint(&mt, 0, nl)];                           /* mcts.py:17 */
+        int f = 0;
+        gain += m3o_apply_action(cfg, seed, n_actions, a, act, b, &mt, &f, 1 << 20);  /* mcts.py:18 */
+        *flags |= f;
+        n_actions--;
+        (*steps)++;
+        memcpy(a, b, sizeof(int32_t) * (size_t)N);
+    }
+    *draws = mt.draws;
+    if (final_board) memcpy(final_board, a, sizeof(int32_t) * (size_t)N);
+    free(a); free(b); free(legal);
+    return gain;
+}
+
+void m3o_batch_rollouts(const m3o_cfg *cfg, int64_t n, const int32_t *boards, const uint32_t *seeds,
+                        const int32_t *n_actions, const uint32_t *rollout_seeds, int nthreads,
+                        int32_t *gain, int32_t *steps, int64_t *draws, int32_t *flags, int32_t *final_boards) {
+    const int N = cfg->R * cfg->C;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 16)
+    for (int64_t i = 0; i < n; i++) {
+        int st = 0, f = 0;
+        int64_t d = 0;
+        gain[i] = (int32_t)m3o_rollout(cfg, boards + i * N, seeds[i], n_actions[i], rollout_seeds[i],
+                                       final_boards ? final_boards + i * N : NULL, &st, &d, &f);
+        steps[i] = st;
+        draws[i] = d;
+        flags[i] = f;
+    }
+}
+
 int64_t m3o_run_episodes(const m3o_cfg *cfg, int64_t n, const uint32_t *seeds,
                          int num_moves, int env_goal, int nthreads, int64_t *out_total) {
     int64_t steps = 0;

@@ -81,6 +81,20 @@ void m3o_batch_episodes(const m3o_cfg *cfg, int64_t n, const uint32_t *seeds, in
                         int nthreads, int32_t *actions, int32_t *rewards, int32_t *draws, uint8_t *done,
                         int32_t *final_boards, int32_t *moves_out, int32_t *flags_out);
 
+/* MCTS.rollout (mctslib/standard/mcts.py:14-19) from state (board, seed = cfg.seed,
+ * n_actions): np.random.seed(rollout_seed); while n_actions >= 1: action =
+ * choice(legal_actions) on the global stream; board = apply_action(action).
+ * Writes the terminal board (nullable), the step count, the global stream's
+ * draws since its last seed and the OR of the step flags; returns the summed
+ * step rewards (the rollout's return minus state.reward). */
+int64_t m3o_rollout(const m3o_cfg *cfg, const int32_t *board, uint32_t seed, int n_actions,
+                    uint32_t rollout_seed, int32_t *final_board, int *steps, int64_t *draws, int *flags);
+
+/* Threaded: n rollouts (boards [n][R*C]); gain/steps/draws/flags [n], final [n][R*C] nullable. */
+void m3o_batch_rollouts(const m3o_cfg *cfg, int64_t n, const int32_t *boards, const uint32_t *seeds,
+                        const int32_t *n_actions, const uint32_t *rollout_seeds, int nthreads,
+                        int32_t *gain, int32_t *steps, int64_t *draws, int32_t *flags, int32_t *final_boards);
+
 /* Threaded CPU baseline: run n episodes (seeds[i]) of num_moves moves with
  * random actions; returns total env steps; writes per-episode total reward. */
 int64_t m3o_run_episodes(const m3o_cfg *cfg, int64_t n, const uint32_t *seeds,

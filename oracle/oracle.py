@@ -82,6 +82,9 @@ def lib():
         L.m3o_batch_episodes.argtypes = [P(Cfg), ctypes.c_int64, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          i32p, i32p, i32p, u8p, i32p, i32p, i32p]
         L.m3o_batch_episodes.restype = None
+        L.m3o_batch_rollouts.argtypes = [P(Cfg), ctypes.c_int64, i32p, u32p, i32p, u32p, ctypes.c_int,
+                                         i32p, i32p, i64p, i32p, i32p]
+        L.m3o_batch_rollouts.restype = None
         _lib = L
     return _lib
 
@@ -174,6 +177,25 @@ class Oracle:
                                  _p(done, ctypes.c_uint8), _p(final, ctypes.c_int32), _p(moves, ctypes.c_int32),
                                  _p(flags, ctypes.c_int32))
         return dict(actions=acts, rewards=rews, draws=drw, done=done, final=final, moves=moves, flags=flags)
+
+    def rollouts(self, boards, seeds, n_actions, rollout_seeds, threads=None):
+        """MCTS.rollout (mctslib/standard/mcts.py:14-19) for many states at once (OpenMP)."""
+        boards = np.ascontiguousarray(boards, dtype=np.int32).reshape(-1, self.R * self.C)
+        n = boards.shape[0]
+        seeds = np.ascontiguousarray(np.broadcast_to(seeds, (n,)), dtype=np.uint32)
+        n_actions = np.ascontiguousarray(np.broadcast_to(n_actions, (n,)), dtype=np.int32)
+        rollout_seeds = np.ascontiguousarray(np.broadcast_to(rollout_seeds, (n,)), dtype=np.uint32)
+        threads = threads or min(16, os.cpu_count() or 1)
+        gain = np.zeros(n, np.int32)
+        steps = np.zeros(n, np.int32)
+        draws = np.zeros(n, np.int64)
+        flags = np.zeros(n, np.int32)
+        final = np.zeros((n, self.R * self.C), np.int32)
+        lib().m3o_batch_rollouts(ctypes.byref(self.cfg), n, _p(boards, ctypes.c_int32), _p(seeds, ctypes.c_uint32),
+                                 _p(n_actions, ctypes.c_int32), _p(rollout_seeds, ctypes.c_uint32), threads,
+                                 _p(gain, ctypes.c_int32), _p(steps, ctypes.c_int32), _p(draws, ctypes.c_int64),
+                                 _p(flags, ctypes.c_int32), _p(final, ctypes.c_int32))
+        return dict(gain=gain, steps=steps, draws=draws, flags=flags, final=final)
 
     def run_episodes(self, seeds, num_moves=20, env_goal=2**31 - 1, threads=1):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
