@@ -67,7 +67,9 @@ int set_err(int code, const char* fmt, ...) {
 constexpr int BLOCK = 256;
 constexpr int FIX_BLOCK = 64;
 constexpr int FIX_GRID = 16;       // step fixup almost never has work: few blocks schedule fast
-constexpr int INIT_FIX_GRID = 64;  // ~1% of resets: one board per wave
+constexpr int INIT_FIX_GRID = 256;   // resets needing >= 624 draws, one board per lane (16x16)
+constexpr int INIT_FIX_BLOCK = 64;
+constexpr int WAVE_FIX_GRID = 64;    // same, one board per wave (9x9: ~1% of resets)
 constexpr int INIT_BLOCK = 64;
 constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 
@@ -93,7 +95,15 @@ struct KS {
     using RawT = typename SC::RawT;
     static constexpr int TS_WORDS = CF::BITS * TSW;                 // per board in HBM
     static constexpr int LDS_WORDS = CF::BITS * (TSW + 1) + ACCW;   // per lane in LDS (+ zero pad per plane)
-    using Rng = typename SC::Rng;
+#ifndef M3_ENV_CHAIN
+#define M3_ENV_CHAIN 1
+#endif
+    // The env step's RNG: CHAIN = the register-only MT19937 chain from the
+    // board's (seed, mt[397]) -- 4 B of per-board state; otherwise the
+    // per-board stream cache (RAWN raw outputs + tile planes, ~420 B read per
+    // step at 9x9), built by the reset.
+    static constexpr bool CHAIN = M3_ENV_CHAIN != 0;
+    using Rng = std::conditional_t<CHAIN, ChainMT, typename SC::Rng>;
 };
 
 // Per-lane match-group table (see m3_rules.hpp, match_scan): the first CAP
@@ -452,6 +462,7 @@ struct InitArgs {
     void* sraw;
     uint32_t* sts;
     uint32_t* sacc;
+    uint32_t* m397;              // nullable: mt[397] of the seed's init_genrand state at (slot, b)
     int64_t cstride;
 };
 
@@ -517,6 +528,7 @@ __device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t
     ChainMT g;
     g.init(seed, m397);
     const int64_t cb = (int64_t)slot * a.cstride + b;  // cache row of (slot, b)
+    if (a.m397) a.m397[cb] = m397;
     RawT* row = a.sraw ? static_cast<RawT*>(a.sraw) + cb * K::RAWN : nullptr;
     uint32_t* sacc = a.sacc ? a.sacc + (int64_t)slot * K::ACCW * a.cstride + b : nullptr;
     uint32_t* sts = a.sts ? a.sts + (int64_t)slot * K::TS_WORDS * a.cstride + b : nullptr;
@@ -669,7 +681,7 @@ __device__ __forceinline__ void wave_fill(uint32_t* key, uint8_t* cells, int lan
 constexpr int WC_WAVES = 4;
 
 template <class CF>
-__global__ void __launch_bounds__(64 * WC_WAVES) k_init_fix(InitArgs a) {
+__global__ void __launch_bounds__(64 * WC_WAVES) k_init_fix_wave(InitArgs a) {
     __shared__ uint32_t key_s[WC_WAVES][624];
     __shared__ __attribute__((aligned(16))) uint8_t cell_s[WC_WAVES][(CF::N + 3) / 4 * 4 + 16];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -708,6 +720,68 @@ __global__ void __launch_bounds__(64 * WC_WAVES) k_init_fix(InitArgs a) {
             for (int x = lane; x < CF::N; x += 64) dst[x] = (int8_t)cells[x];
         }
         wave_sync();
+    }
+}
+
+// ---- lane-per-board reset for boards that need >= 624 draws -------------
+// One board per lane with the full 624-word MT19937 state in lane-private
+// scratch (FullMT; scratch is swizzled per lane, so the state accesses of a
+// wave are coalesced). At 9x9x6 ~0.7% of resets land here, at 16x16x8 ~60%
+// (every round of randint(1, 9, (16, 16)) takes 256 draws), so this pass is
+// throughput work: all 64 lanes of a wave run their own board.
+//
+// One round of BoardV2.__init__ (boardv2.py:21 / :25): randint(1, T+1, (R, C))
+// draws a tile for EVERY cell in row-major order; cells outside `only` take
+// their draw and drop it (array[mask] = new[mask]). A plane word collects 32
+// tiles, then merges under the mask.
+template <class CF, class RNG>
+__device__ __forceinline__ void fill_round(typename CF::Bd* P, RNG& mt, const typename CF::Bd* only) {
+#pragma unroll
+    for (int w = 0; w < CF::W; ++w) {
+        constexpr int BITS = CF::BITS;
+        const int nbits = CF::N - 32 * w < 32 ? CF::N - 32 * w : 32;
+        uint32_t t[BITS];
+#pragma unroll
+        for (int p = 0; p < BITS; ++p) t[p] = 0u;
+        for (int bit = 0; bit < nbits; ++bit) {
+            uint32_t v = 1u;
+            if constexpr (CF::TILE_RNG != 0u) {
+                do {
+                    v = mt.next32() & CF::TILE_MASK;
+                } while (v > CF::TILE_RNG);
+                v += 1u;
+            }
+#pragma unroll
+            for (int p = 0; p < BITS; ++p) t[p] |= ((v >> p) & 1u) << bit;
+        }
+        const uint32_t m = only ? only->w[w] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int p = 0; p < BITS; ++p) P[p].w[w] = (P[p].w[w] & ~m) | (t[p] & m);
+    }
+}
+
+template <class CF>
+__global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
+    const uint32_t cnt = *a.ovf_count;
+    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[1], cnt);
+    for (uint32_t oi = blockIdx.x * INIT_FIX_BLOCK + threadIdx.x; oi < cnt; oi += gridDim.x * INIT_FIX_BLOCK) {
+        int64_t b;
+        uint32_t seed, slot;
+        init_item(a, (int64_t)a.ovf_list[oi], b, seed, slot);
+        FullMT mt;
+        mt.init(seed, 0u);
+        const uint32_t m397 = mt.key[397];  // init_genrand state, before the first twist
+        typename CF::Bd P[CF::NP], mask;
+#pragma unroll
+        for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+        fill_round<CF>(P, mt, nullptr);                              // boardv2.py:21
+        while (get_match_mask<CF>(P, mask)) fill_round<CF>(P, mt, &mask);  // boardv2.py:23-27
+        const int64_t ob = (int64_t)slot * a.sstride + b;
+        init_outputs<CF>(a, b, ob, seed, m397, mt.draws(), P);
+        constexpr int NW = (CF::N + 3) / 4;
+        uint32_t cw[NW];
+        words_from_planes<CF>(P, cw);
+        init_store_board<CF>(a, ob, cw);
     }
 }
 
@@ -770,9 +844,10 @@ struct EnvArgs {
     uint32_t* pf_list;   // prefetch queue of this step: board, seed, slot
     uint32_t* pf_seed;
     uint32_t* pf_slot;
-    const void* sraw;    // stream caches of the 3 slots (layout: InitArgs)
+    const void* sraw;    // stream caches of the NSLOT slots (layout: InitArgs; KS::CHAIN: unused)
     const uint32_t* sts;
     const uint32_t* sacc;
+    const uint32_t* m397;  // [NSLOT][cstride] mt[397] of each slot's seed (KS::CHAIN)
     int64_t cstride;
 };
 
@@ -864,15 +939,14 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
     uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
     uint32_t* const gtab = stage_tab;
-    __shared__ uint32_t cache_s[K::LDS_WORDS * K::B];
+    __shared__ uint32_t cache_s[K::CHAIN ? 1 : K::LDS_WORDS * K::B];
     const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
     const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
     block_copy_in<CF::N, KS<CF>::B>(a.cur + b0 * CF::N, lds, nb);
     const int t = threadIdx.x;
-    uint32_t cslot = 0u;
-    if (t < nb) {  // this lane's tile planes (+ zero pad) and acceptance words, lane-interleaved
+    const uint32_t cslot = t < nb ? a.slot[b0 + t] : 0u;
+    if (!K::CHAIN && t < nb) {  // this lane's tile planes (+ zero pad) and acceptance words, lane-interleaved
         const int64_t b = b0 + t;
-        cslot = a.slot[b];
         const uint32_t* sts = a.sts + (int64_t)cslot * K::TS_WORDS * a.cstride + b;
         const uint32_t* sacc = a.sacc + (int64_t)cslot * K::ACCW * a.cstride + b;
 #pragma unroll
@@ -905,8 +979,11 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
         typename CF::Bd P[CF::NP];
         lds_to_planes<CF>(lds, t, P);
         typename K::Rng rng;
-        rng.init(static_cast<const typename K::RawT*>(a.sraw) + ((int64_t)cslot * a.cstride + b) * K::RAWN,
-                 cache_s + t, cache_s + CF::BITS * (K::TSW + 1) * K::B + t, K::B);
+        if constexpr (K::CHAIN)
+            rng.init(a.seeds[b], a.m397[(int64_t)cslot * a.cstride + b]);
+        else
+            rng.init(static_cast<const typename K::RawT*>(a.sraw) + ((int64_t)cslot * a.cstride + b) * K::RAWN,
+                     cache_s + t, cache_s + CF::BITS * (K::TSW + 1) * K::B + t, K::B);
         if (!env_step_one<CF>(P, a, b, rng, st)) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
             a.ovf_list[slot] = (uint32_t)b;
@@ -1126,6 +1203,7 @@ struct m3_env {
     uint32_t* ne_legal = nullptr;
     void* sraw = nullptr;
     uint32_t *sts = nullptr, *sacc = nullptr;
+    uint32_t* m397 = nullptr;  // [NSLOT][n]
     // prefetch queues and their overflow lists, by step % PF_LAG
     uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {}, *pf_ovf[PF_LAG] = {};
     int64_t steps = 0;
@@ -1205,7 +1283,10 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_init_fix<CF>, dim3(INIT_FIX_GRID), dim3(64 * WC_WAVES), 0, stream, a);
+    if constexpr (CF::N > 128)  // most resets overflow the first MT block: throughput pass
+        hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3(INIT_FIX_GRID), dim3(INIT_FIX_BLOCK), 0, stream, a);
+    else  // ~1%: latency pass
+        hipLaunchKernelGGL(k_init_fix_wave<CF>, dim3(WAVE_FIX_GRID), dim3(64 * WC_WAVES), 0, stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }
@@ -1228,9 +1309,12 @@ void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
     r.board_words = e->ne_words + o * ((CF::N + 3) / 4);
     r.first_action = e->ne_first + o;
     r.legal = e->ne_legal + o * CF::AW;
-    r.sraw = static_cast<typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
-    r.sts = e->sts + o;
-    r.sacc = e->sacc + o;
+    if constexpr (!KS<CF>::CHAIN) {
+        r.sraw = static_cast<typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
+        r.sts = e->sts + o;
+        r.sacc = e->sacc + o;
+    }
+    r.m397 = e->m397 + o;
     r.cstride = e->n;
 }
 
@@ -1283,9 +1367,15 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.pf_list = e->pf_list[par] + o;
     a.pf_seed = e->pf_seed[par] + o;
     a.pf_slot = e->pf_slot[par] + o;
-    a.sraw = static_cast<const typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
-    a.sts = e->sts + o;
-    a.sacc = e->sacc + o;
+    if constexpr (!KS<CF>::CHAIN) {
+        a.sraw = static_cast<const typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
+        a.sts = e->sts + o;
+        a.sacc = e->sacc + o;
+    } else {
+        a.sraw = nullptr;
+        a.sts = a.sacc = nullptr;
+    }
+    a.m397 = e->m397 + o;
     a.cstride = e->n;
     HIP_TRY(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
     const bool timed = e->tn < e->tcap;
@@ -1737,9 +1827,12 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         using K = KS<decltype(cf)>;
         using St = LdsStore<decltype(cf), K::GCAP, K::B>;
         alloc(&e->spill, (size_t)MAX_SHARDS * K::SPILL_RECORDS * St::SPILL_WORDS * 4);
-        alloc(&e->sraw, (size_t)NSLOT * n * (size_t)K::RAWN * sizeof(typename K::RawT));
-        alloc(&e->sts, (size_t)NSLOT * n * 4ull * K::TS_WORDS);
-        alloc(&e->sacc, (size_t)NSLOT * n * 4ull * K::ACCW);
+        if constexpr (!K::CHAIN) {
+            alloc(&e->sraw, (size_t)NSLOT * n * (size_t)K::RAWN * sizeof(typename K::RawT));
+            alloc(&e->sts, (size_t)NSLOT * n * 4ull * K::TS_WORDS);
+            alloc(&e->sacc, (size_t)NSLOT * n * 4ull * K::ACCW);
+        }
+        alloc(&e->m397, (size_t)NSLOT * n * 4ull);
         return 0;
     });
     if (err == hipSuccess) err = hipEventCreateWithFlags(&e->gather_ev, hipEventDisableTiming);
@@ -1796,7 +1889,7 @@ int m3_env_destroy(m3_env* e) {
     void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->flags, e->draws, e->legal, e->score, e->moves,
                     e->next_action, e->reward, e->done, e->trunc, e->actions, e->counters, e->ovf_list,
                     e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal, e->sraw, e->sts,
-                    e->sacc, e->spill};
+                    e->sacc, e->spill, e->m397};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < PF_LAG; ++q)
@@ -1840,9 +1933,10 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     a.draws = e->draws;
     a.ovf_count = &e->counters[32];
     a.ovf_list = e->pf_ovf[0];
-    a.sraw = e->sraw;  // episode slot 0
+    a.sraw = e->sraw;  // episode slot 0 (null with KS::CHAIN: no stream cache)
     a.sts = e->sts;
     a.sacc = e->sacc;
+    a.m397 = e->m397;
     a.cstride = e->n;
     HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));  // also clears the stats
     HIP_TRY(hipMemsetAsync(e->slot, 0, e->n, c->stream));
