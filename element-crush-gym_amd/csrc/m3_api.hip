@@ -909,6 +909,7 @@ __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& 
             for (int i = 0; i < CF::AW; ++i) a.legal[b * CF::AW + i] = a.ne_legal[ob * CF::AW + i];
         }
     }
+    mark<PH_RESET>(st);
     // queue the freed slot for the episode after next: one atomic per wave, not per lane
     const uint64_t m = __ballot(reset);
     if (m) {
@@ -923,6 +924,7 @@ __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& 
             a.pf_slot[q] = a.slot[b] == 0u ? (uint32_t)(NSLOT - 1) : a.slot[b] - 1u;
         }
     }
+    mark<PH_QUEUE>(st);
     return true;
 }
 

@@ -27,7 +27,8 @@ namespace m3 {
 // Phase-profiling hooks. A Store type that defines PROF receives mark<K>() at
 // phase boundaries (m3_api.hip builds such a variant with -DM3_PHASE_PROF);
 // for every other Store the calls compile to nothing.
-enum : int { PH_LOAD, PH_SWAP, PH_MATCH, PH_CLEAR, PH_DROP, PH_REFILL, PH_LEGAL, PH_NEXT, PH_STORE, PH_N };
+enum : int { PH_LOAD, PH_SWAP, PH_MATCH, PH_CLEAR, PH_DROP, PH_REFILL, PH_LEGAL, PH_NEXT, PH_RESET, PH_QUEUE,
+             PH_STORE, PH_N };
 template <class S, class = void>
 struct HasProf : std::false_type {};
 template <class S>

@@ -131,7 +131,7 @@ class MCTS:
 
     def __init__(self, state, exploration_weight: float, simulations: int, verbose: bool = False,
                  deterministic: bool = False, leaf_rollouts: int = 1,
-                 rollout_fn: Optional[Callable] = None):
+                 rollout_fn: Optional[Callable] = None, rng=None):
         if leaf_rollouts < 1:
             raise ValueError("leaf_rollouts must be >= 1")
         self._root = Node(state)
@@ -141,10 +141,11 @@ class MCTS:
         self.deterministic = deterministic
         self.leaf_rollouts = leaf_rollouts
         self._rollout_fn = rollout_fn
+        self._rng = random if rng is None else rng     # source of rollout seeds (mcts.py:15)
         self._root.expand()                            # abc/mcts.py:84
 
     def _seed(self, state) -> int:
-        return state.seed if self.deterministic else random.randint(0, SEED_BOUND)
+        return state.seed if self.deterministic else self._rng.randint(0, SEED_BOUND)
 
     def rollout(self, state) -> float:
         """mcts.py:14-19 on the device; with leaf_rollouts > 1 the mean of that many."""
@@ -157,36 +158,85 @@ class MCTS:
             rets = rollouts([state] * len(seeds), seeds)["returns"]
         return int(rets[0]) if len(seeds) == 1 else float(rets.mean())
 
+    # ---- one simulation, split so that many searches can share a launch ------
+    def select_leaf(self) -> Node:
+        """Selection + expansion (abc/mcts.py:94-101)."""
+        node = self._root
+        while not node.state.is_terminal and node.is_fully_expanded:
+            node = node.best_child(node.state.n_actions)
+        if not node.state.is_terminal and not node.is_fully_expanded:
+            node = node.expand()
+        return node
+
+    @staticmethod
+    def backpropagate(node: Node, reward) -> None:
+        while node is not None:                        # abc/mcts.py:106-109
+            node.update(reward)
+            node = node.parent
+
+    def finish(self):
+        """Most-visited root child, root policies, greedy-line value; re-root (abc/mcts.py:115-128)."""
+        root = self._root
+        best_action, best = None, None
+        for a, ch in root.children.items():
+            if best is None or ch.visits > best.visits:
+                best_action, best = a, ch
+        policies = root.policies
+        node = root
+        while not node.state.is_terminal and node.is_fully_expanded:
+            node = node.best_child(0)
+        value = node.state.reward
+        best.parent = None
+        self._root = best
+        return best_action, value, policies
+
     def __call__(self):
         pbar = None
         if self._verbose:
             from tqdm import tqdm
 
             pbar = tqdm(total=self._simulations)
-        root = self._root
         for _ in range(self._simulations):
-            node = root
-            while not node.state.is_terminal and node.is_fully_expanded:   # selection
-                node = node.best_child(node.state.n_actions)
-            if not node.state.is_terminal and not node.is_fully_expanded:  # expansion
-                node = node.expand()
-            reward = self.rollout(node.state)                             # simulation
-            while node is not None:                                       # backpropagation
-                node.update(reward)
-                node = node.parent
+            node = self.select_leaf()
+            self.backpropagate(node, self.rollout(node.state))
             if pbar is not None:
                 pbar.update(1)
-        best_action, best = None, None
-        for a, ch in root.children.items():                               # most visited child
-            if best is None or ch.visits > best.visits:
-                best_action, best = a, ch
-        policies = root.policies
-        node = root
-        while not node.state.is_terminal and node.is_fully_expanded:      # greedy line for the value
-            node = node.best_child(0)
-        value = node.state.reward
-        best.parent = None                                                # re-root on the chosen child
-        self._root = best
         if pbar is not None:
             pbar.close()
-        return best_action, value, policies
+        return self.finish()
+
+
+def search_lockstep(searches: Sequence[MCTS]):
+    """Run one ``__call__`` of every search with the simulations in lockstep.
+
+    Simulation i of all searches shares ONE rollout launch (every search's
+    leaf, in order); each search draws its rollout seed from its own ``rng``,
+    so search g returns what ``searches[g]()`` alone would. All leaves must
+    share a board shape. Returns [(action, value, policies)] per search."""
+    searches = list(searches)
+    if not searches:
+        return []
+    sims = searches[0]._simulations
+    if any(m._simulations != sims for m in searches):
+        raise ValueError("lockstep searches need the same number of simulations")
+    for _ in range(sims):
+        leaves, seeds, owner = [], [], []
+        for gi, m in enumerate(searches):
+            leaf = m.select_leaf()
+            for _k in range(m.leaf_rollouts):
+                leaves.append(leaf)
+                seeds.append(m._seed(leaf.state))
+                owner.append(gi)
+            m._leaf = leaf
+        if searches[0]._rollout_fn is not None:
+            rets = np.asarray(searches[0]._rollout_fn([n.state for n in leaves], seeds))
+        else:
+            rets = rollouts([n.state for n in leaves], seeds)["returns"]
+        pos = 0
+        for m in searches:
+            k = m.leaf_rollouts
+            r = rets[pos:pos + k]
+            pos += k
+            m.backpropagate(m._leaf, int(r[0]) if k == 1 else float(np.mean(r)))
+            m._leaf = None
+    return [m.finish() for m in searches]

@@ -28,7 +28,7 @@ import numpy as np  # noqa: E402
 from match3tile import _native  # noqa: E402
 from match3tile.batched import BatchedMatch3Env  # noqa: E402
 
-PHASES = ["load", "swap", "match", "clear", "drop", "refill", "legal", "next", "store"]
+PHASES = ["load", "swap", "match", "clear", "drop", "refill", "legal", "next", "reset", "queue", "store"]
 
 
 def main():
