@@ -56,17 +56,22 @@ def cpu_baseline(rows, cols, types, moves, goal, seconds):
                       "oracle/m3_oracle.c, OpenMP over episodes"}
 
 
-def load_traffic(shape_tag, boards):
-    """HBM bytes/launch of the step kernel from the committed rocprofv3 PMC summary, if one matches."""
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md: SIMD-32, wave64 over 2 cycles), 2.4 GHz
+VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2
+
+
+def load_profile(shape_tag, boards):
+    """The committed rocprofv3 PMC summary of the step kernel (profiles/traffic.json), if one matches."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
         if t.get("shape") == shape_tag and int(t.get("boards")) == boards:
-            return float(t["hbm_bytes_per_launch"])
+            return t
     except Exception:
         pass
-    return None
+    return {}
 
 
 def bench_rollouts(a):
@@ -202,7 +207,9 @@ def main():
     shard_boards = -(-B // stats["shards"])
     bytes_per_launch = shard_boards * algorithmic_bytes_per_step(rows, cols)
     achieved = bytes_per_launch / avg_kernel_s / 1e9
-    traffic = load_traffic(args.shape, B)
+    prof = load_profile(args.shape, B)
+    traffic = prof.get("hbm_bytes_per_launch")
+    valu = prof.get("valu_insts_per_launch")
     out = {
         "metric": METRIC,
         "value": value,
@@ -242,6 +249,12 @@ def main():
             "boards_per_launch": shard_boards,
             "avg_kernel_ms": avg_kernel_s * 1e3,
             "note": "integer-VALU bound path; HBM roofline per BASELINE/SURVEY §8(d): 183 B per 9x9 env-step",
+            # the resource that binds: VALU issue (wave64 instructions from the committed PMC pass
+            # over the live per-launch time), against the chip's VALU issue peak
+            "valu": None if not valu else {
+                "achieved": valu / avg_kernel_s, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave64 VALU instr/s",
+                "frac": valu / avg_kernel_s / VALU_PEAK_WAVE_INSTR_S, "insts_per_launch": valu,
+                "source": prof.get("source")},
         },
     }
     if world == 1 and not args.no_cpu_baseline:

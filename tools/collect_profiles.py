@@ -39,7 +39,8 @@ open(os.path.join(P, f"{tag}_pmc.txt"), "w").write(pmc)
 agg = collections.defaultdict(list)
 for f in glob.glob(f"{src}/**/*_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "k_env_step" in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
+        if "k_env_step" in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU",
+                                                                       "SQ_INSTS_SALU"):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 fetch = sum(agg["FETCH_SIZE"]) / len(agg["FETCH_SIZE"]) * 1024
 write = sum(agg["WRITE_SIZE"]) / len(agg["WRITE_SIZE"]) * 1024
@@ -49,6 +50,8 @@ traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"], "kernel": "k_
            "fetch_size_bytes": fetch, "write_size_bytes": write,
            "hbm_bytes_per_launch": 2 * fetch + write,
            "bytes_per_board": (2 * fetch + write) / bench["roofline"].get("boards_per_launch", cfg["boards_per_gpu"]),
+           "valu_insts_per_launch": sum(agg["SQ_INSTS_VALU"]) / max(1, len(agg["SQ_INSTS_VALU"])),
+           "salu_insts_per_launch": sum(agg["SQ_INSTS_SALU"]) / max(1, len(agg["SQ_INSTS_SALU"])),
            "source": f"profiles/{tag}_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
            "correction": "2 x FETCH_SIZE (gfx950 wide-read calibration) + WRITE_SIZE"}
 json.dump(traffic, open(os.path.join(P, "traffic.json"), "w"), indent=1)
