@@ -61,13 +61,14 @@ def cpu_baseline(rows, cols, types, moves, goal, seconds):
 VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2
 
 
-def load_profile(shape_tag, boards):
+def load_profile(shape_tag, boards, boards_per_launch):
     """The committed rocprofv3 PMC summary of the step kernel (profiles/traffic.json), if one matches."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("shape") == shape_tag and int(t.get("boards")) == boards:
+        if (t.get("shape") == shape_tag and int(t.get("boards")) == boards
+                and int(t.get("boards_per_launch", -1)) == boards_per_launch):
             return t
     except Exception:
         pass
@@ -149,12 +150,21 @@ def main():
     ap.add_argument("--goal", type=int, default=500)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shards", type=int, default=None, help="board shards (HIP streams) per GPU; default: library's")
+    ap.add_argument("--shards", type=int, default=2,
+                    help="board shards per GPU, each on its own step + prefetch HIP stream (fastest: 2 with "
+                         "--hw-queues >= 8, DESIGN §4)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="diagnostic only: boards stop at done (later steps are terminal no-ops); not the headline")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP reads it at init; <= 32): 2 shards use "
+                         "5 streams (context + 2 x (step, prefetch)), each on its own hardware queue")
     ap.add_argument("--rollouts", action="store_true",
                     help="secondary bench: device MCTS rollouts (f3) instead of the env step")
     args = ap.parse_args()
+    if args.hw_queues is not None:
+        if not 1 <= args.hw_queues <= 32:
+            raise SystemExit("--hw-queues must be in [1, 32]")
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.rollouts:
         return bench_rollouts(args)
 
@@ -207,7 +217,7 @@ def main():
     shard_boards = -(-B // stats["shards"])
     bytes_per_launch = shard_boards * algorithmic_bytes_per_step(rows, cols)
     achieved = bytes_per_launch / avg_kernel_s / 1e9
-    prof = load_profile(args.shape, B)
+    prof = load_profile(args.shape, B, shard_boards)
     traffic = prof.get("hbm_bytes_per_launch")
     valu = prof.get("valu_insts_per_launch")
     out = {
@@ -233,6 +243,7 @@ def main():
             "env_goal": args.goal,
             "parallelism": f"dp{world}",
             "shards_per_gpu": stats["shards"],
+            "hw_queues": args.hw_queues,
             "autoreset": not args.no_autoreset,
         },
         "path_stats": {"autoresets": stats["autoresets"], "reset_recomputes": stats["reset_recomputes"],
@@ -248,6 +259,8 @@ def main():
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "boards_per_launch": shard_boards,
             "avg_kernel_ms": avg_kernel_s * 1e3,
+            # the shards' launches overlap, so per launch understates the whole GPU's rate
+            "aggregate_gbs": value / world * algorithmic_bytes_per_step(rows, cols) / 1e9,
             "note": "integer-VALU bound path; HBM roofline per BASELINE/SURVEY §8(d): 183 B per 9x9 env-step",
             # the resource that binds: VALU issue (wave64 instructions from the committed PMC pass
             # over the live per-launch time), against the chip's VALU issue peak

@@ -103,7 +103,13 @@ struct KS {
     // per-board stream cache (RAWN raw outputs + tile planes, ~420 B read per
     // step at 9x9), built by the reset.
     static constexpr bool CHAIN = M3_ENV_CHAIN != 0;
-    using Rng = std::conditional_t<CHAIN, ChainMT, typename SC::Rng>;
+    // 16x16: one chain level (draws < 227; a step needing more -- a near-full
+    // board refill -- goes to k_env_fix), five fewer VGPRs live through the
+    // cascade, +2.5 %. 9x9: the full three-level chain; the one-level build
+    // came out 16 % slower (A/B gpurun_out/ab3), the register allocation of
+    // the 3-waves/SIMD bound shifts with it.
+    using Chain = std::conditional_t<(CF::N > 128), ChainMT1, ChainMT>;
+    using Rng = std::conditional_t<CHAIN, Chain, typename SC::Rng>;
 };
 
 // Per-lane match-group table (see m3_rules.hpp, match_scan): the first CAP
@@ -1108,7 +1114,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_rollout(Rollout
     if (t < nb) {
         const int64_t b = b0 + t;
         const uint32_t rs = a.rseeds[b], s = a.seeds[b];
-        ChainMT first, rng;
+        typename K::Chain first, rng;  // a step past the chain's reach replays the rollout in k_rollout_fix
         first.init(rs, mt_state397(rs));
         rng.init(s, mt_state397(s));
         if (!rollout_one<CF>(P, a, b, first, rng, st)) {
@@ -1842,10 +1848,12 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         m3_env_destroy(e);
         return set_err(M3_ERR_HIP, "env allocation (%lld boards): %s", (long long)n, hipGetErrorString(err));
     }
-    // default: one shard. Measured at 1,048,576 boards (9x9x6, autoreset):
-    // 1 / 2 / 4 / 8 shards = 1.65 / 1.26 / 1.02 / 0.75 G env-steps/s; the
-    // prefetch stream already keeps resets off the step's critical path, and
-    // more streams than GPU_MAX_HW_QUEUES (4) share hardware queues.
+    // default: one shard. Every shard adds two streams (step + prefetch), and
+    // streams beyond GPU_MAX_HW_QUEUES (HIP default 4) share hardware queues,
+    // so a step queues behind a reset launch. Measured at 1,048,576 boards
+    // (9x9x6, autoreset, gpurun_out/q1-q3): 4 queues: 1 / 2 / 4 shards = 1.75 /
+    // 1.43 / 1.18 G env-steps/s; 8 queues: 1.74 / 1.98 / 1.38 (2 shards fill
+    // each other's kernel tails); one prefetch stream shared by 2 shards: 1.67.
     int rc = m3_env_set_shards(e, 1);
     if (rc) {
         m3_env_destroy(e);
