@@ -26,14 +26,21 @@ static void store_planes(const typename CF::Bd* P, int8_t* b) {
 // One apply_action + next random action, the way the kernels do it: fast
 // path first (ChainMT + a group table of capacity CAP), full recompute
 // (FullMT + ArrayStore) when the fast path reports overflow.
-template <class CF, class Store>
+template <class CF, class Store, class Chain = ChainMT>
 static int step_one(typename CF::Bd* P, const int8_t* board, uint32_t seed, int na, int act, Store& st,
                     uint32_t& f, int32_t& draws, uint32_t* legal, int32_t& next_act, int& recomputed) {
     typename CF::Bd HL, VL;
-    ChainMT rng;
+    Chain rng;
     rng.init(seed, mt_state397(seed));
     int r = apply_action<CF>(P, na, act, rng, f, HL, VL, st);
     uint32_t act_bits[CF::AW];
+    int32_t nx = -1;
+    const int32_t step_draws = (int32_t)rng.draws();  // apply_action's draws, before the next choice
+    if (!(f & FLAG_RECOMPUTE) && !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION))) {
+        action_bits<CF>(HL, VL, act_bits);
+        nx = random_action<CF>(act_bits, rng);  // the next action's draws may pass the chain's reach too
+        if (rng.overflow) f |= FLAG_RNG_OVERFLOW;
+    }
     if (f & FLAG_RECOMPUTE) {
         recomputed++;
         FullMT* fm = new FullMT;
@@ -47,9 +54,9 @@ static int step_one(typename CF::Bd* P, const int8_t* board, uint32_t seed, int 
         delete fm;
         delete as;
     } else {
-        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)rng.draws();
         action_bits<CF>(HL, VL, act_bits);
-        next_act = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act_bits, rng);
+        next_act = nx;
+        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : step_draws;
     }
     if (legal) memcpy(legal, act_bits, sizeof(act_bits));
     return r;
@@ -130,7 +137,11 @@ static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const in
         load_planes<CF>(boards + i * CF::N, P);
         uint32_t f;
         uint32_t* lg = legal ? legal + i * CF::AW : nullptr;
-        if (small == 16) {  // batched env path: stream cache + CachedRNG
+        if (small == 32) {  // the 16x16 env step: one-level MT chain (< 227 draws) + the 4-group table
+            SmallStore<CF, 4> ss;
+            rew[i] = step_one<CF, SmallStore<CF, 4>, ChainMT1>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss,
+                                                              f, draws[i], lg, next_act[i], recomputed);
+        } else if (small == 16) {  // batched env path: stream cache + CachedRNG
             rew[i] = step_cached<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], f, draws[i], lg,
                                      next_act[i], recomputed);
         } else if (small == 8) {  // the 9x9 device table size

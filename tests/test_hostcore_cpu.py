@@ -156,3 +156,18 @@ def test_stream_cache_path_random_states(tag):
     b = hc.apply(boards, seeds, 20, acts, small=16)
     for x, y in zip(a, b):
         assert (x == y).all()
+
+
+def test_one_level_chain_fallback_is_exact(golden):
+    """The 16x16 env step runs the one-level MT chain (draws < 227): steps past it -- near-full-board
+    refills such as mega+mega (256 cells) -- must be redone exactly (rare-branch test, forced by the
+    golden combo cases)."""
+    hc = HostCore(16, 16, 8)
+    st = golden("steps")
+    args = (st["board_16x16x8"], st["seed_16x16x8"], st["n_actions_16x16x8"], st["action_16x16x8"])
+    a = hc.apply(*args)
+    b = hc.apply(*args, small=32)
+    assert hc.recomputed > 0
+    for x, y in zip(a, b):
+        assert (x == y).all()
+    _check_steps(hc, st, "16x16x8", 32)
