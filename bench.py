@@ -267,6 +267,8 @@ def main():
             "valu": None if not valu else {
                 "achieved": valu / avg_kernel_s, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave64 VALU instr/s",
                 "frac": valu / avg_kernel_s / VALU_PEAK_WAVE_INSTR_S, "insts_per_launch": valu,
+                # all shards' launches of a step over the step's wall time
+                "aggregate_frac": valu * stats["shards"] / (elapsed / args.steps) / VALU_PEAK_WAVE_INSTR_S,
                 "source": prof.get("source")},
         },
     }
