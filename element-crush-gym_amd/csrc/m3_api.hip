@@ -1,19 +1,19 @@
 // m3_api.hip -- gfx950 kernels + the C ABI of include/m3.h.
 //
-// Kernel shape (all step kernels): one board per lane, 256-lane workgroups
-// (4 wave64s). Boards are int8 [n][R*C] in HBM. A workgroup stages its 256
-// boards (256*81 = 20,736 B at 9x9) HBM -> LDS with 16-byte coalesced loads;
-// each lane reads its own board out of LDS as dwords and transposes it into 7
-// bit-planes in VGPRs, runs the whole fixed-point step in registers
-// (m3_rules.hpp), writes the result back into its LDS slot, and the
-// workgroup streams the 256 boards out with 16-byte stores. Per-board scalars
-// (seed, mt[397], score, moves, pre-drawn action) are SoA and coalesced.
+// Kernel shape (all step kernels): one board per lane, one-wave (64-lane)
+// workgroups. Boards are int8 [n][R*C] in HBM. A wave stages its 64 boards
+// HBM -> LDS with 16-byte coalesced loads; each lane reads its own board out
+// of LDS as dwords and transposes it into 7 bit-planes in VGPRs, runs the
+// whole fixed-point step in registers (m3_rules.hpp), writes the result back
+// into its LDS slot, and the wave streams the boards out with 16-byte stores.
+// Per-board scalars (seed, mt[397], score, moves, pre-drawn action) are SoA
+// and coalesced.
 //
-// The step uses ChainMT (register-only MT19937). A step that needs >= 624
-// draws (never observed in play; possible in principle) appends its index to
-// an overflow list and is redone by k_*_fix with the 624-word FullMT in
-// scratch. That kernel reads the untouched input buffer (boards ping-pong),
-// so the result is still exact.
+// The step's MT19937 is a register-only chain (m3_rng.hpp, ChainMT). A step
+// that needs more draws than the chain reaches, or more match groups than the
+// LDS table + spill pool hold, appends its index to an overflow list and is
+// redone by k_*_fix with the 624-word FullMT in scratch. That kernel reads the
+// untouched input buffer (boards ping-pong), so the result is still exact.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -1307,10 +1307,7 @@ int launch_legal(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* legal) {
     return M3_OK;
 }
 
-// Enqueue one env step of shard s on its stream: zero the shard's counters,
-// k_env_step (cur -> nxt), k_env_fix (recompute overflowed boards), and with
-// autoreset k_init + k_init_fix over the boards that finished. Every pointer
-// is offset to the shard, so kernels see shard-local board indices.
+// InitArgs of the prefetch (next-episode slots) of the boards from offset o.
 template <class CF>
 void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
     r.sstride = e->n;
@@ -1363,7 +1360,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.flags = e->flags + o;
     a.draws = e->draws + o;
     a.legal = e->legal + o * AW;
-    a.packed = e->packed + o;
+    a.packed = e->comm ? e->packed + o : nullptr;  // only the RCCL gather reads it
     a.counters = cnt;
     a.spill = e->spill + (size_t)s * KS<CF>::SPILL_RECORDS * LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::SPILL_WORDS;
     a.stats = base + 16;

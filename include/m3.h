@@ -120,8 +120,10 @@ int m3_env_reset(m3_env *env, const uint32_t *seeds, uint32_t seed_base);
 
 /* Split the boards into nshards (1..8) contiguous shards, each stepped on its
  * own HIP stream (plus one prefetch stream per shard for the autoreset
- * launches). Results do not depend on it. Default: 1 (fastest measured: the
- * prefetch stream already overlaps resets with the single step launch). */
+ * launches). Results do not depend on it. Default: 1. Each shard adds two
+ * streams; with GPU_MAX_HW_QUEUES >= 8 in the process, 2 shards are fastest
+ * (the shards' step kernels fill each other's tails); with HIP's default 4
+ * queues, 1. */
 int m3_env_set_shards(m3_env *env, int nshards);
 /* Wait for all work of the env (every shard stream). */
 int m3_env_synchronize(m3_env *env);
@@ -158,7 +160,9 @@ int m3_comm_unique_id(uint8_t out_id[128]);
 int m3_env_comm_init(m3_env *env, const uint8_t id[128], int nranks, int rank);
 /* ncclAllGather of packed (reward << 2 | truncated << 1 | done) int32 for every
  * board of every rank into a device buffer [nranks][n]; optionally copied to
- * host_out (int32[nranks*n]). Enqueued on the env's stream. */
+ * host_out (int32[nranks*n]). Enqueued on the env's stream. The step kernel
+ * writes the packed words only once a communicator exists, so gather the
+ * outcomes of steps taken after m3_env_comm_init. */
 int m3_env_gather(m3_env *env, int32_t *host_out);
 
 /* Cumulative counters since the last m3_env_reset: out[0] steps recomputed on
