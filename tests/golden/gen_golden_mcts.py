@@ -14,7 +14,9 @@ Runs in this container only (the reference never travels). Writes
              since its last seed;
   searches   ``MCTS(state, c, simulations)()`` (mctslib/abc/mcts.py:71-128) on
              9x9x6 roots: Python ``random`` seed, simulations, the returned
-             (action, value, policies) of two consecutive calls.
+             (action, value, policies) of two consecutive calls;
+  greedy     ``samplerTasks.greedy_test`` episodes (greedy_action every move,
+             boardv2.py:209-218) for board seeds 1..32: actions and reward.
 
 Only data is committed -- no reference source.
 """
@@ -128,10 +130,30 @@ def gen_searches(pool):
     return out
 
 
+def _greedy_case(seed):
+    """samplerTasks.greedy_test (samplerTasks.py:17-22) with a fixed board seed."""
+    state = BoardV2(20, BoardConfig(seed=seed))
+    np.random.seed(state.cfg.seed)
+    acts = []
+    while not state.is_terminal:
+        a = state.greedy_action
+        acts.append(int(a))
+        state = state.apply_action(a)
+    return acts, int(state.reward)
+
+
+def gen_greedy(pool):
+    seeds = list(range(1, 33))
+    res = pool.map(_greedy_case, seeds)
+    return {"gr_seed": np.array(seeds), "gr_actions": np.array([r[0] for r in res], dtype=np.int32),
+            "gr_reward": np.array([r[1] for r in res], dtype=np.int64)}
+
+
 def main():
     with Pool(8) as pool:
         out = gen_rollouts(pool)
         out.update(gen_searches(pool))
+        out.update(gen_greedy(pool))
     np.savez_compressed(os.path.join(OUT, "mcts.npz"), **out)
     print({k: v.shape for k, v in out.items()})
 

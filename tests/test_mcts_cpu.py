@@ -111,3 +111,21 @@ def test_leaf_rollouts_average(golden):
     want = [random.randint(0, 2**31 - 1) for _ in range(24)]
     assert [s for batch in seen for s in batch] == want
     assert all(len(b) == 4 for b in seen)
+
+
+def test_oracle_greedy_episodes_match_reference(golden):
+    """samplerTasks.greedy_test (boardv2.py:209-218 every move) restated over the oracle."""
+    g = golden("mcts")
+    o = Oracle(9, 9, 6)
+    for seed, acts, total in zip(g["gr_seed"], g["gr_actions"], g["gr_reward"]):
+        board, _ = o.init_board(int(seed))
+        reward, na = 0, 20
+        for m in range(20):
+            best, best_r, best_b = None, -1, None
+            for a in o.legal_actions(board):
+                nb, r, _, _ = o.apply_action(board, int(seed), a, na)
+                if reward + r > best_r:
+                    best, best_r, best_b = a, reward + r, nb
+            assert best == acts[m]
+            board, reward, na = best_b, best_r, na - 1
+        assert reward == total
