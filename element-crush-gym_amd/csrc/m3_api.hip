@@ -1234,8 +1234,13 @@ struct m3_env {
         bool ppending[PF_LAG] = {};
     };
     std::vector<Shard> shards;
-    hipEvent_t gather_ev = nullptr;
-    bool gather_pending = false;
+    // host-actions upload on the context stream: the next step's shards wait for it
+    hipEvent_t upload_ev = nullptr;
+    bool upload_pending = false;
+    // `packed` is double-buffered by step parity, so the RCCL gather of step t
+    // (context stream) overlaps step t+1; step t+2 waits for it (gev[buffer])
+    hipEvent_t gev[2] = {nullptr, nullptr};
+    bool gpend[2] = {false, false};
 };
 
 namespace {
@@ -1339,7 +1344,9 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     uint32_t* base = e->counters + 64 * s;
     uint32_t* cnt = base + 4 * par;
     hipStream_t st = sh.stream;
-    if (e->gather_pending) HIP_TRY(hipStreamWaitEvent(st, e->gather_ev, 0));  // `packed` still being read
+    const int pb = (int)(e->steps & 1);  // packed buffer of this step
+    if (e->upload_pending) HIP_TRY(hipStreamWaitEvent(st, e->upload_ev, 0));  // host actions in e->actions
+    if (e->gpend[pb]) HIP_TRY(hipStreamWaitEvent(st, e->gev[pb], 0));          // gather of step t-2 still reading
     if (sh.ppending[par]) HIP_TRY(hipStreamWaitEvent(st, sh.pev[par], 0));  // queue + slots of step t - PF_LAG
     EnvArgs a;
     a.n = sh.n;
@@ -1360,7 +1367,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.flags = e->flags + o;
     a.draws = e->draws + o;
     a.legal = e->legal + o * AW;
-    a.packed = e->comm ? e->packed + o : nullptr;  // only the RCCL gather reads it
+    a.packed = e->comm ? e->packed + (size_t)pb * e->n + o : nullptr;  // only the RCCL gather reads it
     a.counters = cnt;
     a.spill = e->spill + (size_t)s * KS<CF>::SPILL_RECORDS * LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::SPILL_WORDS;
     a.stats = base + 16;
@@ -1421,7 +1428,8 @@ int launch_env_step(m3_env* e, const int32_t* d_actions) {
         int rc = launch_env_shard<CF>(e, s, d_actions);
         if (rc) return rc;
     }
-    e->gather_pending = false;
+    e->upload_pending = false;
+    e->gpend[e->steps & 1] = false;
     e->cur ^= 1;
     e->steps++;
     return M3_OK;
@@ -1817,7 +1825,7 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     alloc(&e->actions, n * 4);
     alloc(&e->counters, 64 * 4 * MAX_SHARDS);
     alloc(&e->ovf_list, n * 4);
-    alloc(&e->packed, n * 4);
+    alloc(&e->packed, 2 * n * 4);
     alloc(&e->slot, n);
     alloc(&e->ne_words, (size_t)NSLOT * n * 4ull * ((c->N + 3) / 4));
     alloc(&e->ne_first, (size_t)NSLOT * n * 4);
@@ -1840,7 +1848,9 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         alloc(&e->m397, (size_t)NSLOT * n * 4ull);
         return 0;
     });
-    if (err == hipSuccess) err = hipEventCreateWithFlags(&e->gather_ev, hipEventDisableTiming);
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&e->upload_ev, hipEventDisableTiming);
+    for (hipEvent_t& ev : e->gev)
+        if (err == hipSuccess) err = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (err != hipSuccess) {
         m3_env_destroy(e);
         return set_err(M3_ERR_HIP, "env allocation (%lld boards): %s", (long long)n, hipGetErrorString(err));
@@ -1892,7 +1902,9 @@ int m3_env_destroy(m3_env* e) {
     (void)hipSetDevice(e->ctx->device);
     (void)sync_env(e);
     destroy_shards(e);
-    if (e->gather_ev) (void)hipEventDestroy(e->gather_ev);
+    if (e->upload_ev) (void)hipEventDestroy(e->upload_ev);
+    for (hipEvent_t ev : e->gev)
+        if (ev) (void)hipEventDestroy(ev);
     void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->flags, e->draws, e->legal, e->score, e->moves,
                     e->next_action, e->reward, e->done, e->trunc, e->actions, e->counters, e->ovf_list,
                     e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal, e->sraw, e->sts,
@@ -1989,8 +2001,8 @@ int m3_env_step(m3_env* e, const int32_t* actions) {
         int rc = join_shards(e, st);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(e->actions, actions, e->n * 4, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipEventRecord(e->gather_ev, st));
-        e->gather_pending = true;
+        HIP_TRY(hipEventRecord(e->upload_ev, st));
+        e->upload_pending = true;
         HIP_TRY(hipStreamSynchronize(st));  // `actions` is a caller-owned host buffer
         return m3_env_step_device(e, e->actions);
     }
@@ -2062,9 +2074,12 @@ int m3_env_gather(m3_env* e, int32_t* host_out) {
     HIP_TRY(hipSetDevice(e->ctx->device));
     int rc = join_shards(e, e->ctx->stream);  // every shard's packed words written
     if (rc) return rc;
-    RCCL_TRY(ncclAllGather(e->packed, e->gathered, (size_t)e->n, ncclInt32, e->comm, e->ctx->stream));
-    HIP_TRY(hipEventRecord(e->gather_ev, e->ctx->stream));  // next step must not overwrite `packed` early
-    e->gather_pending = true;
+    if (e->steps == 0) return set_err(M3_ERR_STATE, "m3_env_gather before the first m3_env_step");
+    const int pb = (int)((e->steps - 1) & 1);  // buffer the last step wrote
+    RCCL_TRY(ncclAllGather(e->packed + (size_t)pb * e->n, e->gathered, (size_t)e->n, ncclInt32, e->comm,
+                           e->ctx->stream));
+    HIP_TRY(hipEventRecord(e->gev[pb], e->ctx->stream));  // the step after next must not overwrite it early
+    e->gpend[pb] = true;
     if (host_out) {
         HIP_TRY(hipMemcpyAsync(host_out, e->gathered, (size_t)e->nranks * e->n * 4, hipMemcpyDeviceToHost,
                                e->ctx->stream));
