@@ -51,3 +51,22 @@ def test_rccl_gather_packs_step_outcomes():
         seen_done += int(d.sum())
     env.close()
     assert seen_done >= n  # every board finished at least once (autoreset ran)
+
+
+def test_rccl_gather_async_double_buffer():
+    """Gathers left in flight while later steps run (packed words double-buffered by step parity):
+    every gathered snapshot must be the outcome of the step it followed."""
+    from match3tile.batched import BatchedMatch3Env
+    from match3tile.distributed import pack_outcomes
+
+    n = 70_000
+    env = BatchedMatch3Env(n, 9, 9, 6, num_moves=20, env_goal=300, shards=2)
+    env.init_comm(BatchedMatch3Env.comm_unique_id(), 1, 0)
+    for t in range(12):
+        env.step()
+        if t % 3 == 2:  # synchronous check every third step
+            g = env.gather(to_host=True)
+            assert (g == pack_outcomes(env.rewards(), env.truncateds(), env.dones())).all(), t
+        else:
+            env.gather()  # async: the next step runs while this gather reads its buffer
+    env.close()
