@@ -69,7 +69,10 @@ constexpr int FIX_BLOCK = 64;
 constexpr int FIX_GRID = 16;       // step fixup almost never has work: few blocks schedule fast
 constexpr int INIT_FIX_GRID = 256;   // resets needing >= 624 draws, one board per lane (16x16)
 constexpr int INIT_FIX_BLOCK = 64;
-constexpr int WAVE_FIX_GRID = 64;    // same, one board per wave (9x9: ~1% of resets)
+#ifndef M3_WAVE_FIX_GRID
+#define M3_WAVE_FIX_GRID 64
+#endif
+constexpr int WAVE_FIX_GRID = M3_WAVE_FIX_GRID;  // same, one board per wave (9x9: ~1% of resets)
 constexpr int INIT_BLOCK = 64;
 constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 
