@@ -173,8 +173,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     rows, cols, types = (int(x) for x in args.shape.split("x"))
 
-    if not os.path.exists(os.path.join(PKG, "build", "libm3.so")):
-        subprocess.run(["make", "-C", PKG], check=True)
+    # no-op when libm3.so is up to date with its sources and compile flags (build/flags.stamp);
+    # A/B variants are separate files (make variant), selected with M3_LIB
+    subprocess.run(["make", "-s", "-C", PKG], check=True)
     from match3tile.batched import BatchedMatch3Env
     from match3tile.distributed import seed_plan, timed_steps
 

@@ -113,6 +113,17 @@ struct KS {
     // the 3-waves/SIMD bound shifts with it.
     using Chain = std::conditional_t<(CF::N > 128), ChainMT1, ChainMT>;
     using Rng = std::conditional_t<CHAIN, Chain, typename SC::Rng>;
+#ifndef M3_CASCADE_LIMIT
+#define M3_CASCADE_LIMIT 2
+#endif
+    // k_env_step runs at most this many cascade iterations per step (-1: no
+    // bound); longer steps are finished by k_env_cont (see there)
+    static constexpr int CASCADE_LIMIT = M3_CASCADE_LIMIT;
+#ifndef M3_ENV_WF
+#define M3_ENV_WF 0
+#endif
+    // the env step as the multi-kernel pipeline k_wf_* (else k_env_step + k_env_cont)
+    static constexpr bool WAVEFRONT = M3_ENV_WF != 0;
 };
 
 // Per-lane match-group table (see m3_rules.hpp, match_scan): the first CAP
@@ -842,7 +853,9 @@ struct EnvArgs {
     uint32_t* draws;
     uint32_t* legal;  // nullable
     int32_t* packed;  // nullable: reward<<2 | trunc<<1 | done for the RCCL gather
-    uint32_t* counters;  // this step's block: [0] overflow count, [1] prefetch count, [3] spill records used
+    uint32_t* counters;  // this step's block: [0] overflow count, [1] prefetch count, [2] prefetch overflow
+                         // count, [3] spill records used, [4] continuation records (k_wf_*: of
+                         // k_wf_begin), [5] [6] of the k_wf_pass passes, [7] dead boards
     uint32_t* spill;     // group-table spill pool of the shard
     uint32_t* stats;     // [0] step recomputes
     uint32_t* ovf_list;
@@ -858,21 +871,24 @@ struct EnvArgs {
     const uint32_t* sacc;
     const uint32_t* m397;  // [NSLOT][cstride] mt[397] of each slot's seed (KS::CHAIN)
     int64_t cstride;
+    uint32_t* cont;        // nullable: continuation records of paused steps (k_env_cont), [1 + WORDS][cont_stride]
+    int64_t cont_stride;
+    // multi-kernel step (k_wf_*): a second record buffer and the settled state
+    // of every board, [EnvCont::WORDS][cont_stride] by board
+    uint32_t* cont2;
+    uint32_t* settled;
+    uint32_t* dead_list;  // boards k_wf_finish found dead (counters[7] of them)
 };
 
-// Match3Env.step bookkeeping (env.py:48-56) around BoardV2.apply_action, and
-// the same-step autoreset (the finished step's reward/done/flags stay visible,
-// the observation and episode state become the next episode's).
+// Match3Env.step bookkeeping (env.py:48-56) after BoardV2.apply_action (r, f,
+// HL/VL of the resulting board), and the same-step autoreset (the finished
+// step's reward/done/flags stay visible, the observation and episode state
+// become the next episode's). mv / sc0: the board's moves and score before the
+// step. Returns false if the next random action ran past the RNG (recompute).
 template <class CF, class RNG, class Store>
-__device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st) {
-    // every per-board input is loaded before the cascade, so its latency hides behind it
-    const int act_in = a.actions ? a.actions[b] : a.next_action[b];
-    const int mv = a.moves[b];
-    const int sc0 = a.score[b];
-    typename CF::Bd HL, VL;
-    uint32_t f;
-    const int r = apply_action<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st);
-    if (f & FLAG_RECOMPUTE) return false;
+__device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
+                                           int r, uint32_t f, const typename CF::Bd& HL, const typename CF::Bd& VL,
+                                           int mv, int sc0) {
     const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
     const int sc = sc0 + r;
     const int mv1 = mv + 1;
@@ -937,6 +953,33 @@ __device__ __forceinline__ bool env_step_one(typename CF::Bd* P, const EnvArgs& 
     return true;
 }
 
+enum : int { ENV_STEP_DONE = 0, ENV_STEP_RECOMPUTE = 1, ENV_STEP_PAUSED = 2 };
+
+// One Match3Env.step of board b. limit >= 0 bounds the cascade (inner
+// iterations): a step that needs more returns ENV_STEP_PAUSED with its state
+// in P, rng, r, f and has written nothing yet; k_env_cont finishes it.
+template <class CF, class RNG, class Store>
+__device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
+                                            int limit, int& r, uint32_t& f) {
+    // every per-board input is loaded before the cascade, so its latency hides behind it
+    const int act_in = a.actions ? a.actions[b] : a.next_action[b];
+    const int mv = a.moves[b];
+    const int sc0 = a.score[b];
+    typename CF::Bd HL, VL;
+    if (apply_begin<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st, r) &&
+        !apply_cascade<CF>(P, rng, f, HL, VL, st, r, limit))
+        return ENV_STEP_PAUSED;
+    if (f & FLAG_RECOMPUTE) return ENV_STEP_RECOMPUTE;
+    return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0) ? ENV_STEP_DONE : ENV_STEP_RECOMPUTE;
+}
+
+// Continuation records of paused steps (KS::CASCADE_LIMIT): word 0 the
+// shard-local board index, words 1.. the Cont state; word w of record q at
+// cont[w * cont_stride + q] (consecutive records of a wave are consecutive
+// dwords). cont_count (the step's counter block [4]) counts them.
+template <class CF>
+using EnvCont = Cont<CF, typename KS<CF>::Rng>;
+
 template <class CF>
 __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArgs a) {
     // The board staging area is only live before the cascade (HBM -> LDS ->
@@ -995,17 +1038,74 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
         else
             rng.init(static_cast<const typename K::RawT*>(a.sraw) + ((int64_t)cslot * a.cstride + b) * K::RAWN,
                      cache_s + t, cache_s + CF::BITS * (K::TSW + 1) * K::B + t, K::B);
-        if (!env_step_one<CF>(P, a, b, rng, st)) {
+        int r;
+        uint32_t f;
+        const int res = env_step_one<CF>(P, a, b, rng, st, a.cont ? K::CASCADE_LIMIT : -1, r, f);
+        if (res == ENV_STEP_RECOMPUTE) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
             a.ovf_list[slot] = (uint32_t)b;
         }
-        planes_to_bytes<CF>(P, lds + t * CF::N);
+        // paused steps leave a continuation record (one atomic per wave)
+        const bool paused = res == ENV_STEP_PAUSED;
+        const uint64_t m = __ballot(paused);
+        if (m) {
+            const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (paused) {
+                const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                uint32_t* rec = a.cont + q;
+                const int64_t cs = a.cont_stride;
+                rec[0] = (uint32_t)b;
+                EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
+            }
+        }
+        planes_to_bytes<CF>(P, lds + t * CF::N);  // a paused board's bytes are rewritten by k_env_cont
     }
     __syncthreads();
     block_copy_out<CF::N, KS<CF>::B>(a.nxt + b0 * CF::N, lds, nb);
 #ifdef M3_PHASE_PROF
     if (live) st.end(0);
 #endif
+}
+
+// Finish the steps k_env_step paused (their cascade ran past KS::CASCADE_LIMIT
+// inner iterations): the long cascades of a launch, packed densely into waves
+// instead of holding every lane of their k_env_step wave idle. Grid-stride
+// over the records; each board is written straight to nxt.
+template <class CF>
+__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_cont(EnvArgs a) {
+    using K = KS<CF>;
+    __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
+    const uint32_t cnt = a.counters[4];
+    LdsStore<CF, K::GCAP, K::B> st{tab + threadIdx.x};
+    st.spill = a.spill;
+    st.pool_next = &a.counters[3];
+    st.pool_cap = K::SPILL_RECORDS;
+    const int64_t cs = a.cont_stride;
+    for (uint32_t q = blockIdx.x * K::B + threadIdx.x; q < cnt; q += gridDim.x * K::B) {
+        const uint32_t* rec = a.cont + q;
+        const int64_t b = rec[0];
+        typename CF::Bd P[CF::NP];
+        typename K::Rng rng;
+        int r;
+        uint32_t f;
+        EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
+        const int mv = a.moves[b], sc0 = a.score[b];
+        typename CF::Bd HL, VL;
+        apply_cascade<CF>(P, rng, f, HL, VL, st, r, -1);
+        const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0);
+        if (!ok) {
+            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+            a.ovf_list[slot] = (uint32_t)b;
+        } else {
+            constexpr int NW = (CF::N + 3) / 4;
+            uint32_t cw[NW];
+            words_from_planes<CF>(P, cw);
+            store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.nxt + b * CF::N), cw);
+        }
+    }
 }
 
 template <class CF>
@@ -1019,8 +1119,242 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
         FullMT mt;  // scratch (see k_apply_fix)
         mt.init(a.seeds[b], 0u);
         ArrayStore<CF> st;
-        env_step_one<CF>(P, a, b, mt, st);
+        int r;
+        uint32_t f;
+        env_step_one<CF>(P, a, b, mt, st, -1, r, f);
         planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * CF::N));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Multi-kernel env step ("wavefront"): the same Match3Env.step as k_env_step,
+// cut at the cascade's iteration boundaries so that every launch runs one
+// coherent piece of work on one board per lane, with its live state in HBM
+// between launches (HBM bandwidth is the resource this path has in plenty):
+//   k_wf_begin   all boards, natural order: swap, combos, first match + clear,
+//                first cascade iteration;
+//   k_wf_pass    the boards still matching, compacted: one more iteration
+//                (twice), then the rest of the cascade (tail, ~8 %);
+//   k_wf_finish  all boards, natural order: legal set, next seeded random
+//                action, Match3Env bookkeeping, autoreset swap, board bytes;
+//   k_env_fix    exact recompute of every board flagged on the way (RNG past
+//                the chain, group-table overflow, dead board: the shuffle).
+// Each kernel holds only its own phase's registers (the megakernel peaks at
+// ~220 VGPRs where legal masks, cascade and shuffle meet), so more waves fit a
+// SIMD, and no lane idles through another board's longer cascade.
+// Board b's settled state: settled[w * cont_stride + b], w < EnvCont::WORDS
+// (flags word FW: FLAG_RECOMPUTE set = k_env_fix owns the board this step).
+// ---------------------------------------------------------------------------
+template <class CF>
+struct WF {
+    using K = KS<CF>;
+    using C = EnvCont<CF>;
+    static constexpr int FW = C::WORDS - 1;  // flags word of a settled state
+#ifndef M3_WF_WPS
+#define M3_WF_WPS 4
+#endif
+    static constexpr int WPS = CF::N > 128 ? 1 : M3_WF_WPS;  // waves per SIMD the wf kernels are bounded for
+#ifndef M3_WF_BEGIN_LIMIT
+#define M3_WF_BEGIN_LIMIT 2
+#endif
+#ifndef M3_WF_PASSES
+#define M3_WF_PASSES 0
+#endif
+    static constexpr int BEGIN_LIMIT = M3_WF_BEGIN_LIMIT;  // cascade iterations in k_wf_begin
+    static constexpr int PASSES = M3_WF_PASSES;            // one-iteration k_wf_pass launches before the tail
+    static_assert(BEGIN_LIMIT >= 1 && PASSES >= 0 && PASSES <= 2, "record counters [4 .. 6]");
+};
+
+template <class CF>
+__device__ __forceinline__ void wf_settle(const EnvArgs& a, int64_t b, const typename CF::Bd* P,
+                                          const typename KS<CF>::Rng& rng, int r, uint32_t f) {
+    const int64_t cs = a.cont_stride;
+    EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { a.settled[(int64_t)i * cs + b] = w; });
+}
+
+__device__ __forceinline__ void wf_recompute(const EnvArgs& a, int64_t b, uint32_t f, int fw) {
+    a.settled[(int64_t)fw * a.cont_stride + b] = f | FLAG_RNG_OVERFLOW;  // any FLAG_RECOMPUTE bit
+    const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+    a.ovf_list[slot] = (uint32_t)b;
+}
+
+// ballot-compacted continuation record (one atomic per wave)
+template <class CF>
+__device__ __forceinline__ void wf_push(const EnvArgs& a, uint32_t* out, uint32_t* count, bool want, int64_t b,
+                                        const typename CF::Bd* P, const typename KS<CF>::Rng& rng, int r,
+                                        uint32_t f) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (want) {
+        const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        uint32_t* rec = out + q;
+        const int64_t cs = a.cont_stride;
+        rec[0] = (uint32_t)b;
+        EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
+    }
+}
+
+// swap, combos, first clear and the first cascade iteration of every board
+template <class CF>
+__global__ void __launch_bounds__(KS<CF>::B, WF<CF>::WPS) k_wf_begin(EnvArgs a) {
+    using K = KS<CF>;
+    constexpr int STAGE_WORDS = (K::B * CF::N + 16 + 3) / 4;
+    constexpr int TAB_WORDS = LdsStore<CF, K::GCAP, K::B>::WORDS;
+    // staging (read once, before the table is first written) aliases the group table
+    __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
+    uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
+    const int64_t b0 = (int64_t)blockIdx.x * K::B;
+    const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
+    block_copy_in<CF::N, K::B>(a.cur + b0 * CF::N, lds, nb);
+    __syncthreads();
+    const int t = threadIdx.x;
+    LdsStore<CF, K::GCAP, K::B> st{stage_tab + t};
+    st.spill = a.spill;
+    st.pool_next = &a.counters[3];
+    st.pool_cap = K::SPILL_RECORDS;
+    if (t >= nb) return;
+    const int64_t b = b0 + t;
+    typename CF::Bd P[CF::NP];
+    lds_to_planes<CF>(lds, t, P);
+    const uint32_t cslot = a.slot[b];
+    typename K::Rng rng;
+    rng.init(a.seeds[b], a.m397[(int64_t)cslot * a.cstride + b]);
+    const int act_in = a.actions ? a.actions[b] : a.next_action[b];
+    const int mv = a.moves[b];
+    int r;
+    uint32_t f;
+    typename CF::Bd HL, VL;
+    int cs = CAS_SETTLED;
+    if (apply_begin<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st, r, false))
+        cs = apply_cascade_ex<CF>(P, rng, f, HL, VL, st, r, WF<CF>::BEGIN_LIMIT, true, false);
+    const bool redo = (f & FLAG_RECOMPUTE) != 0;
+    const bool paused = !redo && cs == CAS_PAUSED;
+    if (redo) wf_recompute(a, b, f, WF<CF>::FW);
+    else if (!paused) wf_settle<CF>(a, b, P, rng, r, f);
+    wf_push<CF>(a, a.cont, &a.counters[4], paused, b, P, rng, r, f);
+}
+
+// one more cascade iteration (limit 1) or the rest of it (limit -1) of the
+// records in rin (count *cin); still-matching boards go to rout (*cout)
+template <class CF>
+__global__ void __launch_bounds__(KS<CF>::B, WF<CF>::WPS) k_wf_pass(EnvArgs a, const uint32_t* rin,
+                                                                      const uint32_t* cin, uint32_t* rout,
+                                                                      uint32_t* cout, int limit) {
+    using K = KS<CF>;
+    __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
+    const uint32_t cnt = *cin;
+    LdsStore<CF, K::GCAP, K::B> st{tab + threadIdx.x};
+    st.spill = a.spill;
+    st.pool_next = &a.counters[3];
+    st.pool_cap = K::SPILL_RECORDS;
+    const int64_t cs = a.cont_stride;
+    for (uint32_t q0 = blockIdx.x * K::B; q0 < cnt; q0 += gridDim.x * K::B) {
+        const uint32_t q = q0 + threadIdx.x;
+        const bool live = q < cnt;
+        int64_t b = 0;
+        typename CF::Bd P[CF::NP];
+        typename K::Rng rng;
+        int r = 0;
+        uint32_t f = 0;
+        bool paused = false;
+        if (live) {
+            const uint32_t* rec = rin + q;
+            b = rec[0];
+            EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
+            typename CF::Bd HL, VL;
+            const int c = apply_cascade_ex<CF>(P, rng, f, HL, VL, st, r, limit, true, false);
+            const bool redo = (f & FLAG_RECOMPUTE) != 0;
+            paused = !redo && c == CAS_PAUSED;
+            if (redo) wf_recompute(a, b, f, WF<CF>::FW);
+            else if (!paused) wf_settle<CF>(a, b, P, rng, r, f);
+        }
+        if (rout) wf_push<CF>(a, rout, cout, paused, b, P, rng, r, f);
+    }
+}
+
+// legal set, next seeded random action, bookkeeping, autoreset swap and the
+// board bytes of every board
+template <class CF>
+__global__ void __launch_bounds__(KS<CF>::B, WF<CF>::WPS) k_wf_finish(EnvArgs a) {
+    using K = KS<CF>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[K::B * CF::N + 16];
+    const int64_t b0 = (int64_t)blockIdx.x * K::B;
+    const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
+    const int t = threadIdx.x;
+    if (t < nb) {
+        const int64_t b = b0 + t;
+        const int64_t cs = a.cont_stride;
+        uint32_t f = a.settled[(int64_t)WF<CF>::FW * cs + b];
+        typename CF::Bd P[CF::NP];
+#pragma unroll
+        for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+        if (!(f & FLAG_RECOMPUTE)) {  // else k_env_fix writes this board
+            typename K::Rng rng;
+            int r;
+            const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
+            if (stepped) {
+                EnvCont<CF>::load(P, rng, r, f, [&](int i) { return a.settled[(int64_t)i * cs + b]; });
+            } else {  // the board is unchanged: its bytes (all 7 planes) are the input
+                bytes_to_planes<CF>(a.cur + b * CF::N, P);
+                rng.init(0u, 0u);
+                r = 0;
+            }
+            const int mv = a.moves[b], sc0 = a.score[b];
+            typename CF::Bd HL, VL;
+            legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
+            NoStore ns;
+            if (stepped && !(HL.any() || VL.any())) {  // dead board: the shuffle path, k_wf_dead
+                const uint32_t slot = atomicAdd(&a.counters[7], 1u);
+                a.dead_list[slot] = (uint32_t)b;
+            } else if (!env_finish<CF>(P, a, b, rng, ns, r, f, HL, VL, mv, sc0)) {
+                const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+                a.ovf_list[slot] = (uint32_t)b;
+            }
+        }
+        planes_to_bytes<CF>(P, lds + t * CF::N);
+    }
+    __syncthreads();
+    block_copy_out<CF::N, K::B>(a.nxt + b0 * CF::N, lds, nb);
+}
+
+// Dead boards (no legal move once settled: ~1e-5 of steps): the row shuffle
+// and whatever follows it (boardv2.py:188-202) from the settled state, on the
+// same register MT chain -- a few lanes, one small grid, instead of the
+// FullMT recompute.
+template <class CF>
+__global__ void __launch_bounds__(KS<CF>::B) k_wf_dead(EnvArgs a) {
+    using K = KS<CF>;
+    __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
+    const uint32_t cnt = a.counters[7];
+    LdsStore<CF, K::GCAP, K::B> st{tab + threadIdx.x};
+    st.spill = a.spill;
+    st.pool_next = &a.counters[3];
+    st.pool_cap = K::SPILL_RECORDS;
+    const int64_t cs = a.cont_stride;
+    for (uint32_t q = blockIdx.x * K::B + threadIdx.x; q < cnt; q += gridDim.x * K::B) {
+        const int64_t b = a.dead_list[q];
+        typename CF::Bd P[CF::NP];
+        typename K::Rng rng;
+        int r;
+        uint32_t f;
+        EnvCont<CF>::load(P, rng, r, f, [&](int i) { return a.settled[(int64_t)i * cs + b]; });
+        const int mv = a.moves[b], sc0 = a.score[b];
+        typename CF::Bd HL, VL;
+        apply_cascade_ex<CF>(P, rng, f, HL, VL, st, r, -1, false, true);
+        const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0);
+        if (!ok) {
+            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+            a.ovf_list[slot] = (uint32_t)b;
+        } else {
+            constexpr int NW = (CF::N + 3) / 4;
+            uint32_t cw[NW];
+            words_from_planes<CF>(P, cw);
+            store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.nxt + b * CF::N), cw);
+        }
     }
 }
 
@@ -1199,10 +1533,20 @@ struct m3_env {
     uint32_t *seeds = nullptr, *flags = nullptr, *draws = nullptr, *legal = nullptr;
     int32_t *score = nullptr, *moves = nullptr, *next_action = nullptr, *reward = nullptr;
     uint8_t *done = nullptr, *trunc = nullptr;
-    int32_t* actions = nullptr;
-    // counters, 64 words per shard: [4q + 0] step overflow count, [4q + 1]
-    // prefetch queue length, [4q + 2] prefetch overflow count (q = step % PF_LAG);
-    // stats [16] step recomputes, [17] resets, [18] reset recomputes
+    // host-action steps (m3_env_step with actions): device copies and pinned
+    // staging, double-buffered by step parity like `packed`, uploaded on
+    // `ustream` (allocated on first use)
+    int32_t* actions[2] = {nullptr, nullptr};
+    int32_t* hstage[2] = {nullptr, nullptr};
+    hipStream_t ustream = nullptr;
+    hipEvent_t upload_ev[2] = {nullptr, nullptr};
+    bool upload_pend[2] = {false, false};  // upload_ev[p] recorded and not yet waited on by the host
+    bool upload_this = false;              // the step being enqueued reads actions[step & 1]
+    // counters, 64 words per shard: [8q + 0] step overflow count, [8q + 1]
+    // prefetch queue length, [8q + 2] prefetch overflow count, [8q + 3] spill
+    // records taken, [8q + 4] continuation records (q = step % PF_LAG); stats
+    // [40] step recomputes, [41] resets, [42] reset recomputes; [48 + k] the
+    // reset / slot-fill overflow counts (shard 0's block)
     uint32_t* counters = nullptr;
     uint32_t* ovf_list = nullptr;
     uint32_t* spill = nullptr;  // group-table spill pools, one per shard slot
@@ -1215,6 +1559,10 @@ struct m3_env {
     void* sraw = nullptr;
     uint32_t *sts = nullptr, *sacc = nullptr;
     uint32_t* m397 = nullptr;  // [NSLOT][n]
+    uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont, k_wf_*)
+    uint32_t* cont2 = nullptr;    // second record buffer (k_wf_pass)
+    uint32_t* settled = nullptr;  // settled state of every board [EnvCont::WORDS][n] (k_wf_*)
+    uint32_t* dead_list = nullptr;  // [n] (k_wf_dead)
     // prefetch queues and their overflow lists, by step % PF_LAG
     uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {}, *pf_ovf[PF_LAG] = {};
     int64_t steps = 0;
@@ -1233,13 +1581,12 @@ struct m3_env {
         int64_t off = 0, n = 0;
         hipStream_t stream = nullptr, pstream = nullptr;
         hipEvent_t ev = nullptr;       // last step work of this shard
+        hipEvent_t aev[2] = {};        // step work of the last step of each parity (reads actions[parity])
+        bool apending[2] = {};
         hipEvent_t pev[PF_LAG] = {};   // prefetch of queue q done
         bool ppending[PF_LAG] = {};
     };
     std::vector<Shard> shards;
-    // host-actions upload on the context stream: the next step's shards wait for it
-    hipEvent_t upload_ev = nullptr;
-    bool upload_pending = false;
     // `packed` is double-buffered by step parity, so the RCCL gather of step t
     // (context stream) overlaps step t+1; step t+2 waits for it (gev[buffer])
     hipEvent_t gev[2] = {nullptr, nullptr};
@@ -1332,7 +1679,9 @@ void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
 }
 
 // Enqueue one env step of shard s: on the step stream, wait for the prefetch
-// of two steps ago, zero this parity's counters, k_env_step (cur -> nxt, with
+// of step t - PF_LAG (the queue and slots this step reuses), for the RCCL
+// gather of step t - 2 (same `packed` buffer) and, for host actions, for
+// their upload; zero this parity's counters, k_env_step (cur -> nxt, with
 // the in-step autoreset swap) and k_env_fix (exact recompute of overflowed
 // boards); on the prefetch stream, k_init + k_init_fix over the queued slots.
 // Every pointer is offset to the shard, so kernels see shard-local indices.
@@ -1345,11 +1694,13 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     const int N = c->N, AW = c->AW;
     const int par = (int)(e->steps % PF_LAG);
     uint32_t* base = e->counters + 64 * s;
-    uint32_t* cnt = base + 4 * par;
+    uint32_t* cnt = base + 8 * par;
     hipStream_t st = sh.stream;
     const int pb = (int)(e->steps & 1);  // packed buffer of this step
-    if (e->upload_pending) HIP_TRY(hipStreamWaitEvent(st, e->upload_ev, 0));  // host actions in e->actions
+    if (e->upload_this) HIP_TRY(hipStreamWaitEvent(st, e->upload_ev[pb], 0));  // host actions in actions[pb]
+#ifndef M3_TEST_NO_GATHER_WAIT  // negative-control build for tests/test_gpu_dist.py only
     if (e->gpend[pb]) HIP_TRY(hipStreamWaitEvent(st, e->gev[pb], 0));          // gather of step t-2 still reading
+#endif
     if (sh.ppending[par]) HIP_TRY(hipStreamWaitEvent(st, sh.pev[par], 0));  // queue + slots of step t - PF_LAG
     EnvArgs a;
     a.n = sh.n;
@@ -1373,7 +1724,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.packed = e->comm ? e->packed + (size_t)pb * e->n + o : nullptr;  // only the RCCL gather reads it
     a.counters = cnt;
     a.spill = e->spill + (size_t)s * KS<CF>::SPILL_RECORDS * LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::SPILL_WORDS;
-    a.stats = base + 16;
+    a.stats = base + 40;
     a.ovf_list = e->ovf_list + o;
     a.slot = e->slot + o;
     a.ne_words = e->ne_words + o * ((N + 3) / 4);
@@ -1392,18 +1743,58 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     }
     a.m397 = e->m397 + o;
     a.cstride = e->n;
-    HIP_TRY(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
+    a.cont = (KS<CF>::WAVEFRONT || KS<CF>::CASCADE_LIMIT >= 0) ? e->cont + o : nullptr;
+    a.cont2 = KS<CF>::WAVEFRONT ? e->cont2 + o : nullptr;
+    a.settled = KS<CF>::WAVEFRONT ? e->settled + o : nullptr;
+    a.dead_list = KS<CF>::WAVEFRONT ? e->dead_list + o : nullptr;
+    a.cont_stride = e->n;
+    HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), st));
     const bool timed = e->tn < e->tcap;
     if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], st));
-    hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
-    HIP_TRY(hipGetLastError());
-    if (timed) {
+    // launches that grid-stride over a device-side count are sized for its usual share of the shard
+    auto frac_grid = [&](double f) {
+        const int64_t g = ((int64_t)(sh.n * f) + KS<CF>::B - 1) / KS<CF>::B;
+        return dim3((unsigned)(g > 0 ? g : 1));
+    };
+    if constexpr (KS<CF>::WAVEFRONT) {
+        // records: begin -> cont, each one-iteration pass -> the other buffer, the tail finishes them;
+        // share of boards still matching after k iterations: 1: ~50 %, 2: ~19 %, 3: ~8 %
+        static constexpr double share[5] = {1.0, 0.6, 0.3, 0.15, 0.08};
+        hipLaunchKernelGGL(k_wf_begin<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
+        HIP_TRY(hipGetLastError());
+        uint32_t* rb[2] = {a.cont, a.cont2};
+        int k = WF<CF>::BEGIN_LIMIT, p = 0;
+        for (; p < WF<CF>::PASSES; ++p, ++k) {
+            hipLaunchKernelGGL(k_wf_pass<CF>, frac_grid(share[k < 4 ? k : 4]), dim3(KS<CF>::B), 0, st, a, rb[p & 1],
+                               &cnt[4 + p], rb[(p + 1) & 1], &cnt[5 + p], 1);
+            HIP_TRY(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_wf_pass<CF>, frac_grid(share[k < 4 ? k : 4]), dim3(KS<CF>::B), 0, st, a, rb[p & 1],
+                           &cnt[4 + p], (uint32_t*)nullptr, (uint32_t*)nullptr, -1);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_wf_finish<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_wf_dead<CF>, dim3(1), dim3(KS<CF>::B), 0, st, a);
+        HIP_TRY(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
+        HIP_TRY(hipGetLastError());
+        if (a.cont) {  // sized for the share of paused steps (~20 % at limit 2)
+            hipLaunchKernelGGL(k_env_cont<CF>, frac_grid(0.25), dim3(KS<CF>::B), 0, st, a);
+            HIP_TRY(hipGetLastError());
+        }
+    }
+    if (timed) {  // the step pipeline of the shard, fixup pass excluded
         HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], st));
         e->tn++;
     }
     hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sh.ev, st));
+    if (e->upload_this) {  // the upload two steps ahead rewrites actions[pb] once this shard has read it
+        HIP_TRY(hipEventRecord(sh.aev[pb], st));
+        sh.apending[pb] = true;
+    }
     if (e->autoreset) {
         HIP_TRY(hipStreamWaitEvent(sh.pstream, sh.ev, 0));
         InitArgs r{};
@@ -1414,7 +1805,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.list_count = &cnt[1];
         r.ovf_count = &cnt[2];
         r.ovf_list = e->pf_ovf[par] + o;
-        r.stats = base + 17;
+        r.stats = base + 41;
         prefetch_args<CF>(e, o, r);
         // the grid is sized for the expected number of finished boards and grid-strides
         int rc = launch_init<CF>(sh.pstream, r, sh.n / 8 + 1);
@@ -1431,7 +1822,7 @@ int launch_env_step(m3_env* e, const int32_t* d_actions) {
         int rc = launch_env_shard<CF>(e, s, d_actions);
         if (rc) return rc;
     }
-    e->upload_pending = false;
+    e->upload_this = false;
     e->gpend[e->steps & 1] = false;
     e->cur ^= 1;
     e->steps++;
@@ -1450,7 +1841,10 @@ int sync_env(m3_env* e) {
         HIP_TRY(hipStreamSynchronize(sh.stream));
         HIP_TRY(hipStreamSynchronize(sh.pstream));
         for (bool& p : sh.ppending) p = false;
+        for (bool& p : sh.apending) p = false;
     }
+    if (e->ustream) HIP_TRY(hipStreamSynchronize(e->ustream));
+    e->upload_pend[0] = e->upload_pend[1] = false;
     HIP_TRY(hipStreamSynchronize(e->ctx->stream));
     return M3_OK;
 }
@@ -1461,6 +1855,7 @@ void destroy_shards(m3_env* e) {
         (void)hipStreamDestroy(sh.pstream);
         (void)hipEventDestroy(sh.ev);
         for (hipEvent_t ev : sh.pev) (void)hipEventDestroy(ev);
+        for (hipEvent_t ev : sh.aev) (void)hipEventDestroy(ev);
     }
     e->shards.clear();
 }
@@ -1477,7 +1872,7 @@ int fill_next_slots(m3_env* e) {
         r.seed_add = k * e->stride;
         r.slot0 = k;
         r.slot_of = e->slot;
-        r.ovf_count = &e->counters[32 + k];
+        r.ovf_count = &e->counters[48 + k];
         r.ovf_list = e->pf_ovf[0];
         prefetch_args<CF>(e, 0, r);
         HIP_TRY(hipMemsetAsync(r.ovf_count, 0, 4, c->stream));
@@ -1825,7 +2220,6 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     alloc(&e->reward, n * 4);
     alloc(&e->done, n);
     alloc(&e->trunc, n);
-    alloc(&e->actions, n * 4);
     alloc(&e->counters, 64 * 4 * MAX_SHARDS);
     alloc(&e->ovf_list, n * 4);
     alloc(&e->packed, 2 * n * 4);
@@ -1849,9 +2243,15 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
             alloc(&e->sacc, (size_t)NSLOT * n * 4ull * K::ACCW);
         }
         alloc(&e->m397, (size_t)NSLOT * n * 4ull);
+        constexpr size_t RW = 1 + EnvCont<decltype(cf)>::WORDS;
+        if constexpr (K::WAVEFRONT || K::CASCADE_LIMIT >= 0) alloc(&e->cont, RW * n * 4ull);
+        if constexpr (K::WAVEFRONT) {
+            alloc(&e->cont2, RW * n * 4ull);
+            alloc(&e->settled, (RW - 1) * n * 4ull);
+            alloc(&e->dead_list, n * 4ull);
+        }
         return 0;
     });
-    if (err == hipSuccess) err = hipEventCreateWithFlags(&e->upload_ev, hipEventDisableTiming);
     for (hipEvent_t& ev : e->gev)
         if (err == hipSuccess) err = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (err != hipSuccess) {
@@ -1889,6 +2289,7 @@ int m3_env_set_shards(m3_env* e, int nshards) {
         HIP_TRY(hipStreamCreateWithFlags(&sh.pstream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&sh.ev, hipEventDisableTiming));
         for (hipEvent_t& ev : sh.pev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        for (hipEvent_t& ev : sh.aev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         e->shards.push_back(sh);
     }
     return M3_OK;
@@ -1905,13 +2306,18 @@ int m3_env_destroy(m3_env* e) {
     (void)hipSetDevice(e->ctx->device);
     (void)sync_env(e);
     destroy_shards(e);
-    if (e->upload_ev) (void)hipEventDestroy(e->upload_ev);
+    for (int p = 0; p < 2; ++p) {
+        if (e->upload_ev[p]) (void)hipEventDestroy(e->upload_ev[p]);
+        if (e->hstage[p]) (void)hipHostFree(e->hstage[p]);
+    }
+    if (e->ustream) (void)hipStreamDestroy(e->ustream);
     for (hipEvent_t ev : e->gev)
         if (ev) (void)hipEventDestroy(ev);
     void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->flags, e->draws, e->legal, e->score, e->moves,
-                    e->next_action, e->reward, e->done, e->trunc, e->actions, e->counters, e->ovf_list,
+                    e->next_action, e->reward, e->done, e->trunc, e->actions[0], e->actions[1], e->counters,
+                    e->ovf_list,
                     e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal, e->sraw, e->sts,
-                    e->sacc, e->spill, e->m397};
+                    e->sacc, e->spill, e->m397, e->cont, e->cont2, e->settled, e->dead_list};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < PF_LAG; ++q)
@@ -1953,7 +2359,7 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     a.trunc = e->trunc;
     a.flags = e->flags;
     a.draws = e->draws;
-    a.ovf_count = &e->counters[32];
+    a.ovf_count = &e->counters[48];
     a.ovf_list = e->pf_ovf[0];
     a.sraw = e->sraw;  // episode slot 0 (null with KS::CHAIN: no stream cache)
     a.sts = e->sts;
@@ -1994,22 +2400,40 @@ int m3_env_step_device(m3_env* e, const int32_t* d_actions) {
     return with_shape(e->ctx->shape, [&](auto cf) { return launch_env_step<decltype(cf)>(e, d_actions); });
 }
 
+// Host actions: copied into pinned staging[p] (p = step parity) on the host,
+// uploaded to actions[p] on the upload stream, which waits only for the
+// shards of step t-2 (the last readers of actions[p]) -- not for step t-1 and
+// not for an RCCL gather on the context stream. The host blocks only until
+// the upload of step t-2 has left staging[p].
 int m3_env_step(m3_env* e, const int32_t* actions) {
     CHECK_ARG(e, "null env");
-    if (actions) {
-        // the previous step may still read e->actions: order the upload after
-        // every shard, and every shard of this step after the upload
-        HIP_TRY(hipSetDevice(e->ctx->device));
-        hipStream_t st = e->ctx->stream;
-        int rc = join_shards(e, st);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(e->actions, actions, e->n * 4, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipEventRecord(e->upload_ev, st));
-        e->upload_pending = true;
-        HIP_TRY(hipStreamSynchronize(st));  // `actions` is a caller-owned host buffer
-        return m3_env_step_device(e, e->actions);
+    if (!actions) return m3_env_step_device(e, nullptr);
+    if (!e->ready) return set_err(M3_ERR_STATE, "m3_env_step before m3_env_reset");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    const size_t bytes = (size_t)e->n * 4;
+    if (!e->ustream) {
+        HIP_TRY(hipStreamCreateWithFlags(&e->ustream, hipStreamNonBlocking));
+        for (int p = 0; p < 2; ++p) {
+            HIP_TRY(hipEventCreateWithFlags(&e->upload_ev[p], hipEventDisableTiming));
+            HIP_TRY(hipMalloc(&e->actions[p], bytes));
+            HIP_TRY(hipHostMalloc(&e->hstage[p], bytes, hipHostMallocDefault));
+        }
     }
-    return m3_env_step_device(e, nullptr);
+    const int pb = (int)(e->steps & 1);
+    if (e->upload_pend[pb]) {  // staging[pb] still feeding the upload of step t-2
+        HIP_TRY(hipEventSynchronize(e->upload_ev[pb]));
+        e->upload_pend[pb] = false;
+    }
+    memcpy(e->hstage[pb], actions, bytes);
+    for (auto& sh : e->shards)
+        if (sh.n && sh.apending[pb]) HIP_TRY(hipStreamWaitEvent(e->ustream, sh.aev[pb], 0));
+    HIP_TRY(hipMemcpyAsync(e->actions[pb], e->hstage[pb], bytes, hipMemcpyHostToDevice, e->ustream));
+    HIP_TRY(hipEventRecord(e->upload_ev[pb], e->ustream));
+    e->upload_pend[pb] = true;
+    e->upload_this = true;
+    const int rc = m3_env_step_device(e, e->actions[pb]);
+    e->upload_this = false;
+    return rc;
 }
 
 static int env_field(m3_env* e, int what, void** ptr, size_t* bytes) {
@@ -2026,6 +2450,11 @@ static int env_field(m3_env* e, int what, void** ptr, size_t* bytes) {
         case M3_ENV_LEGAL: *ptr = e->legal; *bytes = n * 4ull * e->ctx->AW; return M3_OK;
         case M3_ENV_SEEDS: *ptr = e->seeds; *bytes = n * 4; return M3_OK;
         case M3_ENV_DRAWS: *ptr = e->draws; *bytes = n * 4; return M3_OK;
+        case M3_ENV_GATHERED:
+            if (!e->gathered) return set_err(M3_ERR_STATE, "M3_ENV_GATHERED before m3_env_comm_init");
+            *ptr = e->gathered;
+            *bytes = (size_t)e->nranks * n * 4;
+            return M3_OK;
         default: return set_err(M3_ERR_INVALID, "unknown env field %d", what);
     }
 }
@@ -2061,33 +2490,73 @@ int m3_comm_unique_id(uint8_t out_id[128]) {
 
 int m3_env_comm_init(m3_env* e, const uint8_t id[128], int nranks, int rank) {
     CHECK_ARG(e && id && nranks >= 1 && rank >= 0 && rank < nranks, "bad arguments");
+    if (e->comm) return set_err(M3_ERR_STATE, "m3_env_comm_init: the env already has a communicator");
     HIP_TRY(hipSetDevice(e->ctx->device));
+    int32_t* g = nullptr;
+    HIP_TRY(hipMalloc(&g, (size_t)nranks * e->n * 4));
     ncclUniqueId uid;
     memcpy(&uid, id, 128);
-    RCCL_TRY(ncclCommInitRank(&e->comm, nranks, uid, rank));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&comm, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        (void)hipFree(g);
+        return set_err(M3_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    e->comm = comm;
+    e->gathered = g;
     e->nranks = nranks;
     e->rank = rank;
-    HIP_TRY(hipMalloc(&e->gathered, (size_t)nranks * e->n * 4));
+    return M3_OK;
+}
+
+// ncclAllGather of the last step's packed words on the context stream into
+// d_out (nullptr: the env's own buffer, M3_ENV_GATHERED).
+static int env_gather(m3_env* e, int32_t* d_out) {
+    if (!e->comm) return set_err(M3_ERR_STATE, "m3_env_gather before m3_env_comm_init");
+    if (e->steps == 0) return set_err(M3_ERR_STATE, "m3_env_gather before the first m3_env_step");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    int rc = join_shards(e, e->ctx->stream);  // every shard's packed words written
+    if (rc) return rc;
+    const int pb = (int)((e->steps - 1) & 1);  // buffer the last step wrote
+    RCCL_TRY(ncclAllGather(e->packed + (size_t)pb * e->n, d_out ? d_out : e->gathered, (size_t)e->n, ncclInt32,
+                           e->comm, e->ctx->stream));
+    HIP_TRY(hipEventRecord(e->gev[pb], e->ctx->stream));  // the step after next must not overwrite it early
+    e->gpend[pb] = true;
     return M3_OK;
 }
 
 int m3_env_gather(m3_env* e, int32_t* host_out) {
     CHECK_ARG(e, "null env");
-    if (!e->comm) return set_err(M3_ERR_STATE, "m3_env_gather before m3_env_comm_init");
-    HIP_TRY(hipSetDevice(e->ctx->device));
-    int rc = join_shards(e, e->ctx->stream);  // every shard's packed words written
+    int rc = env_gather(e, nullptr);
     if (rc) return rc;
-    if (e->steps == 0) return set_err(M3_ERR_STATE, "m3_env_gather before the first m3_env_step");
-    const int pb = (int)((e->steps - 1) & 1);  // buffer the last step wrote
-    RCCL_TRY(ncclAllGather(e->packed + (size_t)pb * e->n, e->gathered, (size_t)e->n, ncclInt32, e->comm,
-                           e->ctx->stream));
-    HIP_TRY(hipEventRecord(e->gev[pb], e->ctx->stream));  // the step after next must not overwrite it early
-    e->gpend[pb] = true;
     if (host_out) {
         HIP_TRY(hipMemcpyAsync(host_out, e->gathered, (size_t)e->nranks * e->n * 4, hipMemcpyDeviceToHost,
                                e->ctx->stream));
         HIP_TRY(hipStreamSynchronize(e->ctx->stream));
     }
+    return M3_OK;
+}
+
+int m3_env_gather_device(m3_env* e, int32_t* d_out) {
+    CHECK_ARG(e, "null env");
+    return env_gather(e, d_out);
+}
+
+}  // extern "C"
+
+// Test hook kernel: one wave sleeping ~`rounds` x 8k cycles.
+__global__ void k_stall(uint32_t rounds) {
+    for (uint32_t i = 0; i < rounds; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+extern "C" {
+
+int m3_env_debug_stall(m3_env* e, uint32_t usec) {
+    CHECK_ARG(e && usec <= 10u * 1000u * 1000u, "bad arguments");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    // s_sleep 127 = 127 x 64 clocks, ~3.4 us at 2.4 GHz
+    hipLaunchKernelGGL(k_stall, dim3(1), dim3(64), 0, e->ctx->stream, (usec + 2u) / 3u);
+    HIP_TRY(hipGetLastError());
     return M3_OK;
 }
 
@@ -2100,9 +2569,9 @@ int m3_env_stats(m3_env* e, uint64_t out[4]) {
     HIP_TRY(hipMemcpy(h.data(), e->counters, h.size() * 4, hipMemcpyDeviceToHost));
     out[0] = out[1] = out[2] = out[3] = 0;
     for (size_t s = 0; s < e->shards.size(); ++s) {
-        out[0] += h[64 * s + 16];  // steps recomputed (cache exhausted or > table groups)
-        out[1] += h[64 * s + 18];  // resets recomputed by the wave-cooperative pass (>= 624 draws)
-        out[2] += h[64 * s + 17];  // autoresets (episodes prefetched)
+        out[0] += h[64 * s + 40];  // steps recomputed (cache exhausted or > table groups)
+        out[1] += h[64 * s + 42];  // resets recomputed by the wave-cooperative pass (>= 624 draws)
+        out[2] += h[64 * s + 41];  // autoresets (episodes prefetched)
     }
     out[3] = e->shards.size();
     return M3_OK;

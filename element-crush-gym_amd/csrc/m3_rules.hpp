@@ -682,24 +682,37 @@ M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng) {
 }
 
 // --------------------------------------------------------------------------
-// BoardV2.apply_action (boardv2.py:43-207)
-// P: NP planes in/out. Returns the step reward; sets flags/draws and the
-// legal masks of the resulting board.
+// BoardV2.apply_action (boardv2.py:43-207), in two parts so a batched kernel
+// can bound the divergent cascade (apply_begin + apply_cascade == apply_action):
+//   apply_begin   :44-136 + the first clear pass (:141-163 on the swap's
+//                 matches / combo window). Returns false when the step is
+//                 complete already (terminal board, bad action: HL/VL set;
+//                 group-table overflow: flagged for recompute).
+//   apply_cascade the fixed point :138-202 from the top of its inner loop.
+//                 With limit >= 0 it stops before starting inner iteration
+//                 limit + 1 and returns false: the whole state is then P
+//                 (planes 0..5; 6 is clear after the first pass), rng, reward
+//                 and flags, and a later apply_cascade(limit = -1) on that
+//                 state finishes the step exactly as one uninterrupted call
+//                 would (the spawn planes are rewritten before each use).
+// P: NP planes in/out; sets flags, the reward and the legal masks of the
+// resulting board.
 // --------------------------------------------------------------------------
 template <class CF, class RNG, class Store>
-M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, uint32_t& flags,
-                       typename CF::Bd& HL, typename CF::Bd& VL, Store& st) {
+M3_HD bool apply_begin(typename CF::Bd* P, int n_actions, int action, RNG& rng, uint32_t& flags,
+                       typename CF::Bd& HL, typename CF::Bd& VL, Store& st, int& reward, bool legal_now = true) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
     constexpr int C = CF::C, R = CF::R, TM = CF::TM;
     constexpr int H = CF::H, V = CF::V, B = CF::B, M = CF::M;
     constexpr Bd VALID = G::valid();
     flags = 0u;
+    reward = 0;
     mark<PH_LOAD>(st);
     if (n_actions < 1 || action < 0 || action >= CF::A) {      // :44-45, KeyError at :48
         flags = (n_actions < 1) ? FLAG_TERMINAL : FLAG_BAD_ACTION;
-        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
-        return 0;
+        if (legal_now) legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);  // else: the caller's
+        return false;
     }
     rng.reseed();                                               // :46
     // decode (boardConfig.py:45-59)
@@ -748,41 +761,69 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
         mark<PH_SWAP>(st);
         if (get_matches<CF>(P, zr, sw, st) == MATCH_OVERFLOW) {
             flags |= FLAG_GROUP_OVERFLOW;
-            return 0;
+            return false;
         }
         mark<PH_MATCH>(st);
     }
     mark<PH_SWAP>(st);
-    int reward = 0;
     // first pass with all 7 planes (input values may exceed 32 until the clip)
     Bd z = zr | VALID.andnot(tb_nonzero<CF>(P));
     z = fire_specials<CF, CF::NP>(P, z);
     reward += score<CF, CF::NP>(P, z);
     merge_clip<CF, CF::NP>(P, z, sw);
     mark<PH_CLEAR>(st);
+    return true;
+}
+
+// apply_cascade_ex: the fixed point with two more entry/exit points for the
+// batched env's multi-kernel step (m3_api.hip, k_wf_*):
+//   stop_settled:  return CAS_SETTLED as soon as the board has no match left,
+//                  before its legal set (the caller computes that elsewhere);
+//   start_settled: the state is such a settled board: continue at its legal
+//                  set (dead-board shuffle and what follows, :188-202).
+// Returns CAS_PAUSED (limit reached), CAS_SETTLED, or CAS_DONE (HL/VL set;
+// or flags ask for a recompute).
+enum : int { CAS_PAUSED = 0, CAS_DONE = 1, CAS_SETTLED = 2 };
+
+template <class CF, class RNG, class Store>
+M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typename CF::Bd& HL,
+                           typename CF::Bd& VL, Store& st, int& reward, int limit, bool stop_settled,
+                           bool start_settled) {
+    using Bd = typename CF::Bd;
+    using G = typename CF::G;
+    constexpr Bd VALID = G::valid();
+    Bd sw[3];
+    int it = 0;
+    bool settled = start_settled;
     for (;;) {                                                  // :138
         Bd mask;
         bool found = false;
-        for (;;) {  // cascade: refill, rematch, clear while matches remain
-            const Bd em = gravity<CF>(P);                       // :166-173
-            mark<PH_DROP>(st);
-            refill<CF>(P, em, rng);
-            mark<PH_REFILL>(st);
-            if (rng.overflow) break;
-            const int mr = get_matches<CF>(P, mask, sw, st);    // :176-181
-            mark<PH_MATCH>(st);
-            if (mr == MATCH_OVERFLOW) {
-                flags |= FLAG_GROUP_OVERFLOW;
-                return 0;
+        if (!settled) {
+            for (;;) {  // cascade: refill, rematch, clear while matches remain
+                if (it == limit) return CAS_PAUSED;             // paused before iteration limit + 1
+                ++it;
+                const Bd em = gravity<CF>(P);                   // :166-173
+                mark<PH_DROP>(st);
+                refill<CF>(P, em, rng);
+                mark<PH_REFILL>(st);
+                if (rng.overflow) break;
+                const int mr = get_matches<CF>(P, mask, sw, st);  // :176-181
+                mark<PH_MATCH>(st);
+                if (mr == MATCH_OVERFLOW) {
+                    flags |= FLAG_GROUP_OVERFLOW;
+                    return CAS_DONE;
+                }
+                if (mr != MATCH_FOUND) break;
+                Bd z = mask | VALID.andnot(tb_nonzero<CF>(P));  // :199 + TB==0 cells
+                z = fire_specials<CF, 6>(P, z);
+                reward += score<CF, 6>(P, z);
+                merge_clip<CF, 6>(P, z, sw);
+                mark<PH_CLEAR>(st);
             }
-            if (mr != MATCH_FOUND) break;
-            z = mask | VALID.andnot(tb_nonzero<CF>(P));        // :199 + TB==0 cells
-            z = fire_specials<CF, 6>(P, z);
-            reward += score<CF, 6>(P, z);
-            merge_clip<CF, 6>(P, z, sw);
-            mark<PH_CLEAR>(st);
+            if (rng.overflow) break;
+            if (stop_settled) return CAS_SETTLED;
         }
-        if (rng.overflow) break;
+        settled = false;
         // no match left: the legal set of the settled board, computed once
         // after the (divergent) cascade so the wave runs it once
         legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
@@ -800,20 +841,77 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
             const int mr = get_matches<CF>(P, mask, sw, st);
             if (mr == MATCH_OVERFLOW) {
                 flags |= FLAG_GROUP_OVERFLOW;
-                return 0;
+                return CAS_DONE;
             }
             found = mr == MATCH_FOUND;
             if (!found) legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
         }
         if (!found) break;                                      // :195-196
-        z = mask | VALID.andnot(tb_nonzero<CF>(P));            // :199 + TB==0 cells
+        Bd z = mask | VALID.andnot(tb_nonzero<CF>(P));         // :199 + TB==0 cells
         z = fire_specials<CF, 6>(P, z);
         reward += score<CF, 6>(P, z);
         merge_clip<CF, 6>(P, z, sw);
         mark<PH_CLEAR>(st);
     }
     if (rng.overflow) flags |= FLAG_RNG_OVERFLOW;
-    return reward;
+    return CAS_DONE;
+}
+
+// true when the step is finished (HL/VL set, or flagged for recompute),
+// false when paused (see apply_begin)
+template <class CF, class RNG, class Store>
+M3_HD bool apply_cascade(typename CF::Bd* P, RNG& rng, uint32_t& flags, typename CF::Bd& HL,
+                         typename CF::Bd& VL, Store& st, int& reward, int limit) {
+    return apply_cascade_ex<CF>(P, rng, flags, HL, VL, st, reward, limit, false, false) != CAS_PAUSED;
+}
+
+// A paused cascade's live state as Cont<CF, RNG>::WORDS 32-bit words: planes
+// 0..5, the RNG struct, reward, flags. put(i, w) / get(i) choose the memory
+// layout (the env kernel writes them SoA, one word column per index).
+template <class CF, class RNG>
+struct Cont {
+    static_assert(std::is_trivially_copyable<RNG>::value && sizeof(RNG) % 4 == 0, "RNG state must be words");
+    static constexpr int PW = 6 * CF::W;
+    static constexpr int RW = (int)(sizeof(RNG) / 4);
+    static constexpr int WORDS = PW + RW + 2;
+    template <class Put>
+    static M3_HD void save(const typename CF::Bd* P, const RNG& rng, int reward, uint32_t flags, Put put) {
+#pragma unroll
+        for (int p = 0; p < 6; ++p)
+#pragma unroll
+            for (int i = 0; i < CF::W; ++i) put(p * CF::W + i, P[p].w[i]);
+        uint32_t r[RW];
+        __builtin_memcpy(r, &rng, sizeof(RNG));
+#pragma unroll
+        for (int i = 0; i < RW; ++i) put(PW + i, r[i]);
+        put(PW + RW, (uint32_t)reward);
+        put(PW + RW + 1, flags);
+    }
+    template <class Get>
+    static M3_HD void load(typename CF::Bd* P, RNG& rng, int& reward, uint32_t& flags, Get get) {
+#pragma unroll
+        for (int p = 0; p < 6; ++p)
+#pragma unroll
+            for (int i = 0; i < CF::W; ++i) P[p].w[i] = get(p * CF::W + i);
+#pragma unroll
+        for (int p = 6; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+        uint32_t r[RW];
+#pragma unroll
+        for (int i = 0; i < RW; ++i) r[i] = get(PW + i);
+        __builtin_memcpy(&rng, r, sizeof(RNG));
+        reward = (int)get(PW + RW);
+        flags = get(PW + RW + 1);
+    }
+};
+
+// Returns the step reward (0 when flags ask for a recompute).
+template <class CF, class RNG, class Store>
+M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, uint32_t& flags,
+                       typename CF::Bd& HL, typename CF::Bd& VL, Store& st) {
+    int reward;
+    if (apply_begin<CF>(P, n_actions, action, rng, flags, HL, VL, st, reward))
+        apply_cascade<CF>(P, rng, flags, HL, VL, st, reward, -1);
+    return (flags & FLAG_RECOMPUTE) ? 0 : reward;
 }
 
 // --------------------------------------------------------------------------

@@ -26,7 +26,7 @@ FLAG_NO_LEGAL = 0x08
 FLAG_SHUFFLED = 0x10
 
 ENV_BOARDS, ENV_REWARD, ENV_DONE, ENV_TRUNCATED, ENV_SCORE, ENV_MOVES, ENV_FLAGS, ENV_NEXT_ACTION, \
-    ENV_LEGAL, ENV_SEEDS, ENV_DRAWS = range(11)
+    ENV_LEGAL, ENV_SEEDS, ENV_DRAWS, ENV_GATHERED = range(12)
 
 # every symbol declared in include/m3.h
 EXPORTS = [
@@ -36,7 +36,8 @@ EXPORTS = [
     "m3_env_create", "m3_env_destroy", "m3_env_reset", "m3_env_set_shards", "m3_env_synchronize",
     "m3_env_set_autoreset", "m3_env_step",
     "m3_env_step_device", "m3_env_get", "m3_env_device_ptr",
-    "m3_comm_unique_id", "m3_env_comm_init", "m3_env_gather", "m3_env_stats", "m3_env_timing",
+    "m3_comm_unique_id", "m3_env_comm_init", "m3_env_gather", "m3_env_gather_device", "m3_env_debug_stall",
+    "m3_env_stats", "m3_env_timing",
     "m3_env_kernel_ms",
 ]
 
@@ -91,6 +92,8 @@ def lib():
             "m3_comm_unique_id": ([vp], i32),
             "m3_env_comm_init": ([vp, vp, i32, i32], i32),
             "m3_env_gather": ([vp, vp], i32),
+            "m3_env_gather_device": ([vp, vp], i32),
+            "m3_env_debug_stall": ([vp, u32], i32),
             "m3_env_stats": ([vp, vp], i32),
             "m3_env_timing": ([vp, i32], i32),
             "m3_env_kernel_ms": ([vp, vp, i32, vp], i32),

@@ -176,3 +176,16 @@ class BatchedMatch3Env:
         out = np.empty(self.nranks * self.n, np.int32) if to_host else None
         check(lib().m3_env_gather(self.handle, ptr(out)))
         return out
+
+    def gather_device(self, device_out_ptr=None):
+        """Enqueue the all-gather into a caller-owned device buffer int32[nranks][n] (None: the env's own,
+        ENV_GATHERED); valid once the env's context stream gets there (synchronize() or any copy-out)."""
+        check(lib().m3_env_gather_device(self.handle, device_out_ptr))
+
+    def gathered(self):
+        """Host copy of the env's gather buffer [nranks * n] (ordered after every enqueued gather)."""
+        return self._get(_native.ENV_GATHERED, np.int32, (self.nranks * self.n,))
+
+    def debug_stall(self, usec: int):
+        """Test hook: idle the context stream (where gathers run) for ~usec."""
+        check(lib().m3_env_debug_stall(self.handle, int(usec)))

@@ -134,7 +134,10 @@ int m3_env_set_autoreset(m3_env *env, int enabled, uint32_t seed_stride);
 
 /* Match3Env.step (env.py:48-56) on every board. actions: host int32[n], or
  * NULL to play each board's seeded env.board.random_action() (README.md:23,
- * samplerTasks.py:13) drawn on device at the end of the previous step. */
+ * samplerTasks.py:13) drawn on device at the end of the previous step.
+ * Host actions are copied into pinned staging before the call returns (the
+ * caller may reuse `actions` at once) and uploaded on a stream of their own;
+ * the call blocks at most until the upload of two steps earlier is done. */
 int m3_env_step(m3_env *env, const int32_t *actions);
 /* Same with actions already in device memory (int32[n]); NULL = random. */
 int m3_env_step_device(m3_env *env, const int32_t *d_actions);
@@ -151,19 +154,32 @@ int m3_env_step_device(m3_env *env, const int32_t *d_actions);
 #define M3_ENV_LEGAL 8       /* uint32[n][words] legal bitset of the current board */
 #define M3_ENV_SEEDS 9       /* uint32[n]  current episode seed               */
 #define M3_ENV_DRAWS 10      /* uint32[n]  raw MT draws of the last step      */
+#define M3_ENV_GATHERED 11   /* int32 [nranks][n] the env's all-gather buffer (after m3_env_comm_init) */
 int m3_env_get(m3_env *env, int what, void *host_out);
 int m3_env_device_ptr(m3_env *env, int what, void **out);
 
 /* ---- multi-GPU: RCCL over xGMI, one process per GPU --------------------- */
 /* 128-byte ncclUniqueId; rank 0 creates it, the caller ships it to all ranks. */
 int m3_comm_unique_id(uint8_t out_id[128]);
+/* One communicator per env; a second call returns M3_ERR_STATE. */
 int m3_env_comm_init(m3_env *env, const uint8_t id[128], int nranks, int rank);
-/* ncclAllGather of packed (reward << 2 | truncated << 1 | done) int32 for every
- * board of every rank into a device buffer [nranks][n]; optionally copied to
- * host_out (int32[nranks*n]). Enqueued on the env's stream. The step kernel
+/* ncclAllGather of the last step's packed (reward << 2 | truncated << 1 | done)
+ * int32 words of every board of every rank into the env's device buffer
+ * M3_ENV_GATHERED ([nranks][n], rank-major); host_out (nullable, int32[nranks*n])
+ * receives a copy and the call then blocks until it is there. The step kernel
  * writes the packed words only once a communicator exists, so gather the
- * outcomes of steps taken after m3_env_comm_init. */
+ * outcomes of steps taken after m3_env_comm_init. No counterpart in the
+ * reference (single host, no collectives): SURVEY.md §8(e). */
 int m3_env_gather(m3_env *env, int32_t *host_out);
+/* Same, into a caller-owned device buffer d_out (int32[nranks][n]; NULL = the
+ * env's buffer), enqueued on the env's context stream without blocking. d_out
+ * holds the step's outcomes once that stream reaches the gather: after
+ * m3_env_synchronize, or for any later m3_env_get / m3_env_gather. Steps keep
+ * running meanwhile (the packed words are double-buffered by step parity). */
+int m3_env_gather_device(m3_env *env, int32_t *d_out);
+/* Test hook: enqueue ~usec of idle GPU time on the env's context stream (the
+ * stream the gathers run on), to hold a gather in flight while later steps run. */
+int m3_env_debug_stall(m3_env *env, uint32_t usec);
 
 /* Cumulative counters since the last m3_env_reset: out[0] steps recomputed on
  * the exact fallback pass (>= 624 MT draws or more match groups than the LDS

@@ -26,13 +26,39 @@ static void store_planes(const typename CF::Bd* P, int8_t* b) {
 // One apply_action + next random action, the way the kernels do it: fast
 // path first (ChainMT + a group table of capacity CAP), full recompute
 // (FullMT + ArrayStore) when the fast path reports overflow.
+// pause >= 0: the env kernel's bounded cascade -- stop before inner
+// iteration pause + 1, serialize the state through Cont into words, restore
+// it into fresh variables and finish the cascade from there.
 template <class CF, class Store, class Chain = ChainMT>
 static int step_one(typename CF::Bd* P, const int8_t* board, uint32_t seed, int na, int act, Store& st,
-                    uint32_t& f, int32_t& draws, uint32_t* legal, int32_t& next_act, int& recomputed) {
+                    uint32_t& f, int32_t& draws, uint32_t* legal, int32_t& next_act, int& recomputed,
+                    int pause = -1, int* paused = nullptr) {
     typename CF::Bd HL, VL;
     Chain rng;
     rng.init(seed, mt_state397(seed));
-    int r = apply_action<CF>(P, na, act, rng, f, HL, VL, st);
+    int r;
+    if (pause < 0) {
+        r = apply_action<CF>(P, na, act, rng, f, HL, VL, st);
+    } else {
+        if (apply_begin<CF>(P, na, act, rng, f, HL, VL, st, r) &&
+            !apply_cascade<CF>(P, rng, f, HL, VL, st, r, pause)) {
+            using K = Cont<CF, Chain>;
+            uint32_t rec[K::WORDS];
+            K::save(P, rng, r, f, [&](int i, uint32_t w) { rec[i] = w; });
+            typename CF::Bd Q[CF::NP];
+            Chain g2;
+            int r2;
+            uint32_t f2;
+            K::load(Q, g2, r2, f2, [&](int i) { return rec[i]; });
+            apply_cascade<CF>(Q, g2, f2, HL, VL, st, r2, -1);
+            memcpy(P, Q, sizeof(Q));
+            rng = g2;
+            r = r2;
+            f = f2;
+            if (paused) ++*paused;
+        }
+        if (f & FLAG_RECOMPUTE) r = 0;
+    }
     uint32_t act_bits[CF::AW];
     int32_t nx = -1;
     const int32_t step_draws = (int32_t)rng.draws();  // apply_action's draws, before the next choice
@@ -127,6 +153,8 @@ static int step_cached(typename CF::Bd* P, const int8_t* board, uint32_t seed, i
     return r;
 }
 
+static long g_paused = 0;  // steps that paused in the bounded-cascade mode (hc_paused)
+
 template <class CF>
 static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const int32_t* nact, const int32_t* acts,
                    int8_t* out, int32_t* rew, int32_t* draws, int32_t* flags, uint32_t* legal, int32_t* next_act,
@@ -137,7 +165,18 @@ static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const in
         load_planes<CF>(boards + i * CF::N, P);
         uint32_t f;
         uint32_t* lg = legal ? legal + i * CF::AW : nullptr;
-        if (small == 32) {  // the 16x16 env step: one-level MT chain (< 227 draws) + the 4-group table
+        if (small >= 100 && small < 120) {  // bounded cascade, paused after small - 100 iterations and resumed
+            SmallStore<CF, 4> ss;
+            int paused = 0;
+            if (CF::N > 128)
+                rew[i] = step_one<CF, SmallStore<CF, 4>, ChainMT1>(P, boards + i * CF::N, seeds[i], nact[i], acts[i],
+                                                                  ss, f, draws[i], lg, next_act[i], recomputed,
+                                                                  small - 100, &paused);
+            else
+                rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,
+                                      next_act[i], recomputed, small - 100, &paused);
+            g_paused += paused;
+        } else if (small == 32) {  // the 16x16 env step: one-level MT chain (< 227 draws) + the 4-group table
             SmallStore<CF, 4> ss;
             rew[i] = step_one<CF, SmallStore<CF, 4>, ChainMT1>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss,
                                                               f, draws[i], lg, next_act[i], recomputed);
@@ -327,6 +366,11 @@ int hc_rounds(int cfg, long n, const int8_t* b, const uint32_t* s, const int32_t
     DISPATCH(cfg, CALL);
 #undef CALL
     return 0;
+}
+long hc_paused(int reset) {
+    const long v = g_paused;
+    if (reset) g_paused = 0;
+    return v;
 }
 uint32_t hc_chain_draw(uint32_t seed, int k) {  // k-th raw output (0-based) via ChainMT
     ChainMT g;

@@ -171,3 +171,36 @@ def test_one_level_chain_fallback_is_exact(golden):
     for x, y in zip(a, b):
         assert (x == y).all()
     _check_steps(hc, st, "16x16x8", 32)
+
+
+@pytest.mark.parametrize("tag", list(SHAPES))
+@pytest.mark.parametrize("pause", [0, 1, 2, 3])
+def test_paused_cascade_resumes_exactly(golden, tag, pause):
+    """The env kernel's bounded cascade: a step paused before inner iteration pause + 1, its state
+    serialized through Cont (the continuation record) and resumed from the words, must give the
+    uninterrupted step's board, reward, draws, flags, legal set and next action -- on every step,
+    shuffle and combo fixture and on random boards with specials."""
+    import ctypes
+
+    R, C, T = SHAPES[tag]
+    hc = HostCore(R, C, T)
+    cases = []
+    for g in (golden("steps"), golden("shuffle")):
+        na = g["n_actions_" + tag] if "n_actions_" + tag in g else np.full(len(g["seed_" + tag]), 20)
+        ok = g["terminates_" + tag].astype(bool) if "terminates_" + tag in g else np.ones(len(na), bool)
+        cases.append((g["board_" + tag][ok], g["seed_" + tag][ok], na[ok], g["action_" + tag][ok]))
+    rng = np.random.default_rng(17 + pause)
+    n = 1500 if R == 9 else 300
+    seeds = rng.integers(1, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    boards, _, _, _ = hc.init(seeds)
+    vals = {"9x9x6": (8, 16, 24, 32, 11, 19, 27, 0), "16x16x8": (16, 32, 48, 64, 19, 35, 0)}[tag]
+    boards = np.where(rng.random((n, R * C)) < 0.05, rng.choice(vals, size=(n, R * C)), boards).astype(np.int8)
+    cases.append((boards, seeds, np.full(n, 20), rng.integers(0, R * (C - 1) * 2, size=n)))
+    lib().hc_paused.restype = ctypes.c_long
+    lib().hc_paused(1)
+    for b, s, na, a in cases:
+        want = hc.apply(b, s, na, a)
+        got = hc.apply(b, s, na, a, small=100 + pause)
+        for x, y in zip(want, got):
+            assert (x == y).all()
+    assert lib().hc_paused(1) > (200 if pause < 2 else 20)  # the pause path really ran
