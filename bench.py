@@ -214,7 +214,7 @@ def main():
     total_steps = world * B * args.steps
     value = total_steps / elapsed
     avg_kernel_s = float(kms.mean()) / 1e3 if len(kms) else float("nan")
-    # one k_env_step launch processes one shard (B / shards boards, contiguous, the last may be short)
+    # one launch of the step pipeline processes one shard (B / shards boards, contiguous, the last may be short)
     shard_boards = -(-B // stats["shards"])
     bytes_per_launch = shard_boards * algorithmic_bytes_per_step(rows, cols)
     achieved = bytes_per_launch / avg_kernel_s / 1e9
@@ -251,7 +251,9 @@ def main():
                        "step_recomputes": stats["step_recomputes"]},
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_env_step",
+            # one shard's step pipeline: k_env_step + k_env_cont (the continuation of the
+            # long cascades), bracketed by HIP events on the shard's stream
+            "kernel": "k_env_step + k_env_cont",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

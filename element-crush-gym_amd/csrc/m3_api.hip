@@ -87,10 +87,17 @@ struct KS {
     static constexpr int B = 64;
     static constexpr int GCAP = 4;                  // match groups in LDS (more spill to a global pool)
 #ifndef M3_STEP_WPS
-#define M3_STEP_WPS 3
+#define M3_STEP_WPS 4
 #endif
     // k_env_step waves per SIMD the register allocation is bounded for
     static constexpr int STEP_WPS = CF::N > 128 ? 1 : M3_STEP_WPS;
+    // k_env_cont: bounded like the step kernel it runs beside (a 2-waves/SIMD
+    // build without spills measured 4 % slower overall: its waves take register
+    // file the other shard's step waves need)
+#ifndef M3_CONT_WPS
+#define M3_CONT_WPS M3_STEP_WPS
+#endif
+    static constexpr int CONT_WPS = CF::N > 128 ? 1 : M3_CONT_WPS;
     static constexpr uint32_t SPILL_RECORDS = 4096;  // spill pool records per shard
     // per-board stream cache of the batched env (m3_rules.hpp, StreamCache)
     using SC = StreamCache<CF>;
@@ -955,10 +962,16 @@ __device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a,
 
 enum : int { ENV_STEP_DONE = 0, ENV_STEP_RECOMPUTE = 1, ENV_STEP_PAUSED = 2 };
 
-// One Match3Env.step of board b. limit >= 0 bounds the cascade (inner
-// iterations): a step that needs more returns ENV_STEP_PAUSED with its state
-// in P, rng, r, f and has written nothing yet; k_env_cont finishes it.
-template <class CF, class RNG, class Store>
+// internal: a continuation record of a settled board with no legal move (the
+// row shuffle comes next), as opposed to one paused before a cascade iteration
+constexpr uint32_t FLAG_CONT_DEAD = 0x80u;
+
+// One Match3Env.step of board b. With DEFER (k_env_step), the cascade stops
+// after `limit` inner iterations and at a dead board (the shuffle path is left
+// out of the kernel): the step returns ENV_STEP_PAUSED with its state in P,
+// rng, r, f (f & FLAG_CONT_DEAD: dead) and has written nothing yet; k_env_cont
+// finishes it. Without DEFER the whole step runs here.
+template <class CF, bool DEFER, class RNG, class Store>
 __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
                                             int limit, int& r, uint32_t& f) {
     // every per-board input is loaded before the cascade, so its latency hides behind it
@@ -966,9 +979,16 @@ __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a
     const int mv = a.moves[b];
     const int sc0 = a.score[b];
     typename CF::Bd HL, VL;
-    if (apply_begin<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st, r) &&
-        !apply_cascade<CF>(P, rng, f, HL, VL, st, r, limit))
-        return ENV_STEP_PAUSED;
+    if (apply_begin<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st, r)) {
+        const int c = apply_cascade_ex<CF, DEFER ? CASX_STOP_DEAD : 0>(P, rng, f, HL, VL, st, r, limit, false);
+        if (!(f & FLAG_RECOMPUTE)) {
+            if (c == CAS_PAUSED) return ENV_STEP_PAUSED;
+            if (c == CAS_DEAD) {
+                f |= FLAG_CONT_DEAD;
+                return ENV_STEP_PAUSED;
+            }
+        }
+    }
     if (f & FLAG_RECOMPUTE) return ENV_STEP_RECOMPUTE;
     return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0) ? ENV_STEP_DONE : ENV_STEP_RECOMPUTE;
 }
@@ -1040,7 +1060,11 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
                      cache_s + t, cache_s + CF::BITS * (K::TSW + 1) * K::B + t, K::B);
         int r;
         uint32_t f;
-        const int res = env_step_one<CF>(P, a, b, rng, st, a.cont ? K::CASCADE_LIMIT : -1, r, f);
+        int res;
+        if constexpr (K::CASCADE_LIMIT >= 0)  // (a.cont is set)
+            res = env_step_one<CF, true>(P, a, b, rng, st, K::CASCADE_LIMIT, r, f);
+        else
+            res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f);
         if (res == ENV_STEP_RECOMPUTE) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
             a.ovf_list[slot] = (uint32_t)b;
@@ -1075,7 +1099,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
 // instead of holding every lane of their k_env_step wave idle. Grid-stride
 // over the records; each board is written straight to nxt.
 template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_cont(EnvArgs a) {
+__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont(EnvArgs a) {
     using K = KS<CF>;
     __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
     const uint32_t cnt = a.counters[4];
@@ -1094,7 +1118,9 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_cont(EnvArg
         EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
         const int mv = a.moves[b], sc0 = a.score[b];
         typename CF::Bd HL, VL;
-        apply_cascade<CF>(P, rng, f, HL, VL, st, r, -1);
+        const bool dead = (f & FLAG_CONT_DEAD) != 0;  // settled with no legal move: continue at the shuffle
+        f &= ~FLAG_CONT_DEAD;
+        apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, -1, dead);
         const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0);
         if (!ok) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
@@ -1121,7 +1147,7 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
         ArrayStore<CF> st;
         int r;
         uint32_t f;
-        env_step_one<CF>(P, a, b, mt, st, -1, r, f);
+        env_step_one<CF, false>(P, a, b, mt, st, -1, r, f);
         planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * CF::N));
     }
 }
@@ -1230,7 +1256,7 @@ __global__ void __launch_bounds__(KS<CF>::B, WF<CF>::WPS) k_wf_begin(EnvArgs a) 
     typename CF::Bd HL, VL;
     int cs = CAS_SETTLED;
     if (apply_begin<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st, r, false))
-        cs = apply_cascade_ex<CF>(P, rng, f, HL, VL, st, r, WF<CF>::BEGIN_LIMIT, true, false);
+        cs = apply_cascade_ex<CF, CASX_STOP_SETTLED>(P, rng, f, HL, VL, st, r, WF<CF>::BEGIN_LIMIT, false);
     const bool redo = (f & FLAG_RECOMPUTE) != 0;
     const bool paused = !redo && cs == CAS_PAUSED;
     if (redo) wf_recompute(a, b, f, WF<CF>::FW);
@@ -1266,7 +1292,7 @@ __global__ void __launch_bounds__(KS<CF>::B, WF<CF>::WPS) k_wf_pass(EnvArgs a, c
             b = rec[0];
             EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
             typename CF::Bd HL, VL;
-            const int c = apply_cascade_ex<CF>(P, rng, f, HL, VL, st, r, limit, true, false);
+            const int c = apply_cascade_ex<CF, CASX_STOP_SETTLED>(P, rng, f, HL, VL, st, r, limit, false);
             const bool redo = (f & FLAG_RECOMPUTE) != 0;
             paused = !redo && c == CAS_PAUSED;
             if (redo) wf_recompute(a, b, f, WF<CF>::FW);
@@ -1344,7 +1370,7 @@ __global__ void __launch_bounds__(KS<CF>::B) k_wf_dead(EnvArgs a) {
         EnvCont<CF>::load(P, rng, r, f, [&](int i) { return a.settled[(int64_t)i * cs + b]; });
         const int mv = a.moves[b], sc0 = a.score[b];
         typename CF::Bd HL, VL;
-        apply_cascade_ex<CF>(P, rng, f, HL, VL, st, r, -1, false, true);
+        apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, -1, true);
         const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0);
         if (!ok) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);

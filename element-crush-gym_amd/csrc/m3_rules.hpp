@@ -775,20 +775,24 @@ M3_HD bool apply_begin(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
     return true;
 }
 
-// apply_cascade_ex: the fixed point with two more entry/exit points for the
-// batched env's multi-kernel step (m3_api.hip, k_wf_*):
-//   stop_settled:  return CAS_SETTLED as soon as the board has no match left,
-//                  before its legal set (the caller computes that elsewhere);
-//   start_settled: the state is such a settled board: continue at its legal
-//                  set (dead-board shuffle and what follows, :188-202).
-// Returns CAS_PAUSED (limit reached), CAS_SETTLED, or CAS_DONE (HL/VL set;
-// or flags ask for a recompute).
-enum : int { CAS_PAUSED = 0, CAS_DONE = 1, CAS_SETTLED = 2 };
+// apply_cascade_ex: the fixed point with more exit/entry points, so batched
+// kernels can leave rare or long work to another launch (m3_api.hip):
+//   OPTS & CASX_STOP_SETTLED  return CAS_SETTLED as soon as the board has no
+//                  match left, before its legal set (the caller computes it);
+//   OPTS & CASX_STOP_DEAD     return CAS_DEAD when the settled board has no
+//                  legal move, before the row shuffle (:188-194) -- the
+//                  shuffle path is then not even compiled into the caller,
+//                  which keeps its register allocation small;
+//   start_settled  the state is a settled board (CAS_SETTLED / CAS_DEAD):
+//                  continue at its legal set.
+// Returns CAS_PAUSED (limit reached), CAS_SETTLED, CAS_DEAD, or CAS_DONE
+// (HL/VL set; or flags ask for a recompute).
+enum : int { CAS_PAUSED = 0, CAS_DONE = 1, CAS_SETTLED = 2, CAS_DEAD = 3 };
+enum : int { CASX_STOP_SETTLED = 1, CASX_STOP_DEAD = 2 };
 
-template <class CF, class RNG, class Store>
+template <class CF, int OPTS, class RNG, class Store>
 M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typename CF::Bd& HL,
-                           typename CF::Bd& VL, Store& st, int& reward, int limit, bool stop_settled,
-                           bool start_settled) {
+                           typename CF::Bd& VL, Store& st, int& reward, int limit, bool start_settled) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
     constexpr Bd VALID = G::valid();
@@ -821,7 +825,7 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
                 mark<PH_CLEAR>(st);
             }
             if (rng.overflow) break;
-            if (stop_settled) return CAS_SETTLED;
+            if constexpr ((OPTS & CASX_STOP_SETTLED) != 0) return CAS_SETTLED;
         }
         settled = false;
         // no match left: the legal set of the settled board, computed once
@@ -829,6 +833,7 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
         legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
         mark<PH_LEGAL>(st);
         if (HL.any() || VL.any()) break;
+        if constexpr ((OPTS & CASX_STOP_DEAD) != 0) return CAS_DEAD;
         int shuffles = 0;                                       // :188-194 dead board
         while (!found && !(HL.any() || VL.any())) {
             if (shuffles >= CF::SHUFFLE_CAP) {
@@ -862,7 +867,7 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
 template <class CF, class RNG, class Store>
 M3_HD bool apply_cascade(typename CF::Bd* P, RNG& rng, uint32_t& flags, typename CF::Bd& HL,
                          typename CF::Bd& VL, Store& st, int& reward, int limit) {
-    return apply_cascade_ex<CF>(P, rng, flags, HL, VL, st, reward, limit, false, false) != CAS_PAUSED;
+    return apply_cascade_ex<CF, 0>(P, rng, flags, HL, VL, st, reward, limit, false) != CAS_PAUSED;
 }
 
 // A paused cascade's live state as Cont<CF, RNG>::WORDS 32-bit words: planes

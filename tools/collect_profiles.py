@@ -6,9 +6,11 @@
 Writes profiles/<round-tag>_bench.json (the bench line), <round-tag>_kernel_stats.csv
 (rocprofv3 --kernel-trace --stats of the same bench command), <round-tag>_pmc.txt
 (per-kernel PMC means, one rocprofv3 pass per counter group) and traffic.json:
-HBM bytes per k_env_step launch = 2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes), the
-factor 2 being MI355X_MICROARCH.md's gfx950 correction for wide coalesced reads
-(FETCH_SIZE reports half of them; narrower accesses are uncalibrated).
+HBM bytes per launch of one shard's step pipeline (k_env_step + k_env_cont, the
+two kernels bench.py's HIP events bracket) = 2 * FETCH_SIZE + WRITE_SIZE (KB ->
+bytes), the factor 2 being MI355X_MICROARCH.md's gfx950 correction for wide
+coalesced reads (FETCH_SIZE reports half of them; narrower accesses are
+uncalibrated).
 """
 import collections
 import csv
@@ -36,22 +38,29 @@ pmc = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.p
                      capture_output=True, text=True, check=True).stdout
 open(os.path.join(P, f"{tag}_pmc.txt"), "w").write(pmc)
 
-agg = collections.defaultdict(list)
+PIPE = ("k_env_step", "k_env_cont")
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{src}/**/*_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "k_env_step" in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU",
-                                                                       "SQ_INSTS_SALU"):
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-fetch = sum(agg["FETCH_SIZE"]) / len(agg["FETCH_SIZE"]) * 1024
-write = sum(agg["WRITE_SIZE"]) / len(agg["WRITE_SIZE"]) * 1024
+        k = [p for p in PIPE if p + "<" in r["Kernel_Name"]]
+        if k and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_SALU"):
+            agg[r["Counter_Name"]][k[0]].append(float(r["Counter_Value"]))
+
+
+def per_launch(counter):  # mean per launch of each pipeline kernel, summed over the pipeline
+    return sum(sum(v) / len(v) for v in agg[counter].values())
+
+
+fetch = per_launch("FETCH_SIZE") * 1024
+write = per_launch("WRITE_SIZE") * 1024
 cfg = bench["config"]
-traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"], "kernel": "k_env_step",
+traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"], "kernel": "k_env_step + k_env_cont",
            "boards_per_launch": bench["roofline"].get("boards_per_launch"),
            "fetch_size_bytes": fetch, "write_size_bytes": write,
            "hbm_bytes_per_launch": 2 * fetch + write,
            "bytes_per_board": (2 * fetch + write) / bench["roofline"].get("boards_per_launch", cfg["boards_per_gpu"]),
-           "valu_insts_per_launch": sum(agg["SQ_INSTS_VALU"]) / max(1, len(agg["SQ_INSTS_VALU"])),
-           "salu_insts_per_launch": sum(agg["SQ_INSTS_SALU"]) / max(1, len(agg["SQ_INSTS_SALU"])),
+           "valu_insts_per_launch": per_launch("SQ_INSTS_VALU"),
+           "salu_insts_per_launch": per_launch("SQ_INSTS_SALU"),
            "source": f"profiles/{tag}_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
            "correction": "2 x FETCH_SIZE (gfx950 wide-read calibration) + WRITE_SIZE"}
 json.dump(traffic, open(os.path.join(P, "traffic.json"), "w"), indent=1)
