@@ -892,10 +892,13 @@ struct EnvArgs {
 // step's reward/done/flags stay visible, the observation and episode state
 // become the next episode's). mv / sc0: the board's moves and score before the
 // step. Returns false if the next random action ran past the RNG (recompute).
+// board_src (nullable): instead of loading the next episode's cells into P,
+// report their word row ob (ne_words[ob * NW ...]; -1 without a reset) so the
+// caller copies them once P is dead (k_env_step: keeps its register peak low).
 template <class CF, class RNG, class Store>
 __device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
                                            int r, uint32_t f, const typename CF::Bd& HL, const typename CF::Bd& VL,
-                                           int mv, int sc0) {
+                                           int mv, int sc0, int64_t* board_src = nullptr) {
     const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
     const int sc = sc0 + r;
     const int mv1 = mv + 1;
@@ -927,10 +930,14 @@ __device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a,
         const uint32_t s_old = a.slot[b], s_new = s_old + 1u == (uint32_t)NSLOT ? 0u : s_old + 1u;
         const int64_t ob = (int64_t)s_new * a.cstride + b;  // slots are strided by the env's n
         const uint32_t seed = a.seeds[b] + a.stride;
-        uint32_t cw[NW];
+        if (board_src) {
+            *board_src = ob;
+        } else {
+            uint32_t cw[NW];
 #pragma unroll
-        for (int q = 0; q < NW; ++q) cw[q] = a.ne_words[ob * NW + q];
-        planes_from_words<CF>(cw, P);
+            for (int q = 0; q < NW; ++q) cw[q] = a.ne_words[ob * NW + q];
+            planes_from_words<CF>(cw, P);
+        }
         a.slot[b] = (uint8_t)s_new;
         a.seeds[b] = seed;
         a.score[b] = 0;
@@ -973,7 +980,7 @@ constexpr uint32_t FLAG_CONT_DEAD = 0x80u;
 // finishes it. Without DEFER the whole step runs here.
 template <class CF, bool DEFER, class RNG, class Store>
 __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
-                                            int limit, int& r, uint32_t& f) {
+                                            int limit, int& r, uint32_t& f, int64_t* board_src = nullptr) {
     // every per-board input is loaded before the cascade, so its latency hides behind it
     const int act_in = a.actions ? a.actions[b] : a.next_action[b];
     const int mv = a.moves[b];
@@ -990,7 +997,7 @@ __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a
         }
     }
     if (f & FLAG_RECOMPUTE) return ENV_STEP_RECOMPUTE;
-    return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0) ? ENV_STEP_DONE : ENV_STEP_RECOMPUTE;
+    return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, board_src) ? ENV_STEP_DONE : ENV_STEP_RECOMPUTE;
 }
 
 // Continuation records of paused steps (KS::CASCADE_LIMIT): word 0 the
@@ -1061,10 +1068,11 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
         int r;
         uint32_t f;
         int res;
+        int64_t reset_src = -1;  // autoreset: the next episode's cells, copied below once P is dead
         if constexpr (K::CASCADE_LIMIT >= 0)  // (a.cont is set)
-            res = env_step_one<CF, true>(P, a, b, rng, st, K::CASCADE_LIMIT, r, f);
+            res = env_step_one<CF, true>(P, a, b, rng, st, K::CASCADE_LIMIT, r, f, &reset_src);
         else
-            res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f);
+            res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f, &reset_src);
         if (res == ENV_STEP_RECOMPUTE) {
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
             a.ovf_list[slot] = (uint32_t)b;
@@ -1086,6 +1094,13 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
             }
         }
         planes_to_bytes<CF>(P, lds + t * CF::N);  // a paused board's bytes are rewritten by k_env_cont
+        if (reset_src >= 0) {
+            constexpr int NW = (CF::N + 3) / 4;
+            uint32_t cw[NW];
+#pragma unroll
+            for (int q = 0; q < NW; ++q) cw[q] = a.ne_words[reset_src * NW + q];
+            store_cells<CF::N>(lds + t * CF::N, cw);
+        }
     }
     __syncthreads();
     block_copy_out<CF::N, KS<CF>::B>(a.nxt + b0 * CF::N, lds, nb);
@@ -1101,6 +1116,9 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
 template <class CF>
 __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont(EnvArgs a) {
     using K = KS<CF>;
+    // The few waves of this kernel are the step's critical path; they share SIMDs with
+    // the other shard's step waves and the resets: issue first (A/B: within noise).
+    __builtin_amdgcn_s_setprio(3);
     __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
     const uint32_t cnt = a.counters[4];
     LdsStore<CF, K::GCAP, K::B> st{tab + threadIdx.x};
@@ -1611,6 +1629,9 @@ struct m3_env {
         bool apending[2] = {};
         hipEvent_t pev[PF_LAG] = {};   // prefetch of queue q done
         bool ppending[PF_LAG] = {};
+        // counter block q already zeroed for its next step: by the reset, or on the
+        // prefetch stream after its last reader (ordered before that step by pev[q])
+        bool czero[PF_LAG] = {};
     };
     std::vector<Shard> shards;
     // `packed` is double-buffered by step parity, so the RCCL gather of step t
@@ -1774,7 +1795,8 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.settled = KS<CF>::WAVEFRONT ? e->settled + o : nullptr;
     a.dead_list = KS<CF>::WAVEFRONT ? e->dead_list + o : nullptr;
     a.cont_stride = e->n;
-    HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), st));
+    if (!sh.czero[par]) HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), st));
+    sh.czero[par] = false;
     const bool timed = e->tn < e->tcap;
     if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], st));
     // launches that grid-stride over a device-side count are sized for its usual share of the shard
@@ -1836,8 +1858,11 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         // the grid is sized for the expected number of finished boards and grid-strides
         int rc = launch_init<CF>(sh.pstream, r, sh.n / 8 + 1);
         if (rc) return rc;
+        // the resets were the block's last readers: zero it here, off the step's critical path
+        HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), sh.pstream));
         HIP_TRY(hipEventRecord(sh.pev[par], sh.pstream));
         sh.ppending[par] = true;
+        sh.czero[par] = true;
     }
     return M3_OK;
 }
@@ -2395,6 +2420,8 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));  // also clears the stats
     HIP_TRY(hipMemsetAsync(e->slot, 0, e->n, c->stream));
     e->steps = 0;
+    for (auto& sh : e->shards)
+        for (bool& z : sh.czero) z = true;  // (the memset above; the reset ends with a sync)
     int rc = with_shape(c->shape, [&](auto cf) {
         int r = launch_init<decltype(cf)>(c->stream, a, e->n);
         if (r == M3_OK && e->autoreset) r = fill_next_slots<decltype(cf)>(e);
