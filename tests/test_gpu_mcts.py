@@ -117,3 +117,23 @@ def test_search_matches_reference(golden):
             assert a == g[f"se{call}_action"][i]
             assert v == g[f"se{call}_value"][i]
             assert np.array_equal(np.array(p), g[f"se{call}_policies"][i][:n])
+
+
+def test_rollouts_through_dead_boards_vs_oracle(ctxs):
+    """Rollouts whose board goes dead mid-rollout (no legal move once settled, ~1e-5 of steps: the
+    row shuffle, boardFunctions.py:16-23, inside the rollout loop): enough rollouts that dozens take
+    that path; every one of them, and a random sample of the rest, equal the oracle's."""
+    o = Oracle(9, 9, 6)
+    c = ctxs["9x9x6"]
+    n = 1 << 18
+    seeds = (np.arange(n, dtype=np.uint64) * 7919 + 11).astype(np.uint32)
+    boards, _, _ = c.init_boards(seeds)
+    rs = (np.arange(n, dtype=np.uint64) * 104729 + 3).astype(np.uint32)
+    got = c.rollouts(boards, seeds, 20, rs, final_boards=True)
+    shuffled = np.flatnonzero(got["flags"] & _native.FLAG_SHUFFLED)
+    assert len(shuffled) >= 5, len(shuffled)
+    idx = np.union1d(shuffled, np.random.default_rng(3).choice(n, 1024, replace=False))
+    want = o.rollouts(boards[idx].reshape(len(idx), -1).astype(np.int32), seeds[idx], 20, rs[idx], threads=16)
+    for k in ("gain", "steps", "draws", "flags"):
+        assert (got[k][idx] == want[k]).all(), k
+    assert (got["final"][idx].reshape(len(idx), -1) == want["final"]).all()
