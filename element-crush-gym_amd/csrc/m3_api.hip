@@ -125,7 +125,9 @@ struct KS {
 #endif
     // k_env_step runs at most this many cascade iterations per step (-1: no
     // bound); longer steps are finished by k_env_cont (see there)
-    static constexpr int CASCADE_LIMIT = M3_CASCADE_LIMIT;
+    // (16x16: off -- its step kernel runs at 1 wave/SIMD either way, and the
+    // continuation launch cost more than it saved: 0.268 vs 0.261 G env-steps/s)
+    static constexpr int CASCADE_LIMIT = CF::N > 128 ? -1 : M3_CASCADE_LIMIT;
 #ifndef M3_ENV_WF
 #define M3_ENV_WF 0
 #endif
