@@ -90,7 +90,10 @@ struct KS {
 #define M3_STEP_WPS 4
 #endif
     // k_env_step waves per SIMD the register allocation is bounded for
-    static constexpr int STEP_WPS = CF::N > 128 ? 1 : M3_STEP_WPS;
+#ifndef M3_STEP_WPS16
+#define M3_STEP_WPS16 1
+#endif
+    static constexpr int STEP_WPS = CF::N > 128 ? M3_STEP_WPS16 : M3_STEP_WPS;
     // k_env_cont: bounded like the step kernel it runs beside (a 2-waves/SIMD
     // build without spills measured 4 % slower overall: its waves take register
     // file the other shard's step waves need)
@@ -127,7 +130,10 @@ struct KS {
     // bound); longer steps are finished by k_env_cont (see there)
     // (16x16: off -- its step kernel runs at 1 wave/SIMD either way, and the
     // continuation launch cost more than it saved: 0.268 vs 0.261 G env-steps/s)
-    static constexpr int CASCADE_LIMIT = CF::N > 128 ? -1 : M3_CASCADE_LIMIT;
+#ifndef M3_CASCADE_LIMIT16
+#define M3_CASCADE_LIMIT16 -1
+#endif
+    static constexpr int CASCADE_LIMIT = CF::N > 128 ? M3_CASCADE_LIMIT16 : M3_CASCADE_LIMIT;
 #ifndef M3_ENV_WF
 #define M3_ENV_WF 0
 #endif
@@ -772,7 +778,21 @@ __device__ __forceinline__ void fill_round(typename CF::Bd* P, RNG& mt, const ty
         uint32_t t[BITS];
 #pragma unroll
         for (int p = 0; p < BITS; ++p) t[p] = 0u;
-        for (int bit = 0; bit < nbits; ++bit) {
+        int bit = 0;
+        if constexpr (CF::TILE_RNG != 0u && CF::TILE_RNG == CF::TILE_MASK) {
+            // T a power of two: every draw is a tile, so a word is nbits consecutive outputs
+            if (mt.bulk_ready((uint32_t)nbits)) {
+#pragma unroll
+                for (int j = 0; j < nbits; ++j) {
+                    const uint32_t v = (mt.bulk_out((uint32_t)j) & CF::TILE_MASK) + 1u;
+#pragma unroll
+                    for (int p = 0; p < BITS; ++p) t[p] |= ((v >> p) & 1u) << j;
+                }
+                mt.bulk_skip((uint32_t)nbits);
+                bit = nbits;
+            }
+        }
+        for (; bit < nbits; ++bit) {
             uint32_t v = 1u;
             if constexpr (CF::TILE_RNG != 0u) {
                 do {

@@ -139,8 +139,19 @@ using ChainMT = ChainMTT<624u>;
 using ChainMT1 = ChainMTT<227u>;
 
 // Textbook MT19937 (numpy mt19937_seed / mt19937_gen / mt19937_next32).
-struct FullMT {
-    uint32_t key[624];
+// Key is the state's storage: KeyArray = lane-private scratch (an LDS column
+// per lane, one wave per CU, measured slower in k_init_fix_lane). The twist
+// carries key[i+1] to the next index and is unrolled so a batch of state
+// loads is in flight at once; bulk_* hand out a run of outputs the same way.
+struct KeyArray {
+    uint32_t w[624];
+    M3_HD uint32_t& operator[](uint32_t p) { return w[p]; }
+    M3_HD uint32_t operator[](uint32_t p) const { return w[p]; }
+};
+
+template <class Key>
+struct MT19937 {
+    Key key;
     uint32_t pos;
     uint32_t k;  // raw outputs since the last reseed
     uint32_t seed;
@@ -161,10 +172,20 @@ struct FullMT {
         k = 0u;
     }
     M3_HD void gen() {
-        uint32_t i = 0;
-        for (; i < 624u - 397u; ++i) key[i] = key[i + 397u] ^ mt_twist(key[i], key[i + 1u]);
-        for (; i < 623u; ++i) key[i] = key[i - 227u] ^ mt_twist(key[i], key[i + 1u]);
-        key[623] = key[396] ^ mt_twist(key[623], key[0]);
+        uint32_t i = 0, cur = key[0];
+#pragma unroll 8
+        for (; i < 624u - 397u; ++i) {
+            const uint32_t nx = key[i + 1u];
+            key[i] = key[i + 397u] ^ mt_twist(cur, nx);
+            cur = nx;
+        }
+#pragma unroll 8
+        for (; i < 623u; ++i) {
+            const uint32_t nx = key[i + 1u];
+            key[i] = key[i - 227u] ^ mt_twist(cur, nx);
+            cur = nx;
+        }
+        key[623] = key[396] ^ mt_twist(cur, key[0]);
         pos = 0u;
     }
     M3_HD uint32_t next32() {
@@ -174,8 +195,19 @@ struct FullMT {
         k += 1u;
         return mt_temper(y);
     }
+    // n consecutive outputs without a twist between them: out(j) = temper(key[pos + j]).
+    M3_HD bool bulk_ready(uint32_t n) {
+        if (pos == 624u) gen();
+        return pos + n <= 624u;
+    }
+    M3_HD uint32_t bulk_out(uint32_t j) { return mt_temper(key[pos + j]); }
+    M3_HD void bulk_skip(uint32_t n) {
+        pos += n;
+        k += n;
+    }
     M3_HD uint32_t draws() const { return k; }
 };
+using FullMT = MT19937<KeyArray>;
 
 // --------------------------------------------------------------------------
 // Per-board stream cache (batched env). Because the reference reseeds with the
