@@ -89,9 +89,10 @@ struct KS {
 #ifndef M3_STEP_WPS
 #define M3_STEP_WPS 4
 #endif
-    // k_env_step waves per SIMD the register allocation is bounded for
+    // k_env_step waves per SIMD the register allocation is bounded for (16x16:
+    // 2, with 708 B of spill, +7 % over 1 once resets stopped binding)
 #ifndef M3_STEP_WPS16
-#define M3_STEP_WPS16 1
+#define M3_STEP_WPS16 2
 #endif
     static constexpr int STEP_WPS = CF::N > 128 ? M3_STEP_WPS16 : M3_STEP_WPS;
     // k_env_cont: bounded like the step kernel it runs beside (a 2-waves/SIMD
@@ -128,8 +129,8 @@ struct KS {
 #endif
     // k_env_step runs at most this many cascade iterations per step (-1: no
     // bound); longer steps are finished by k_env_cont (see there)
-    // (16x16: off -- its step kernel runs at 1 wave/SIMD either way, and the
-    // continuation launch cost more than it saved: 0.268 vs 0.261 G env-steps/s)
+    // (16x16: off -- the continuation launch cost more than it saved:
+    // 0.364 vs 0.337 G env-steps/s at 1 wave/SIMD, 0.391 vs 0.384 at 2)
 #ifndef M3_CASCADE_LIMIT16
 #define M3_CASCADE_LIMIT16 -1
 #endif
@@ -809,17 +810,24 @@ __device__ __forceinline__ void fill_round(typename CF::Bd* P, RNG& mt, const ty
     }
 }
 
-template <class CF>
+// DIRECT: every reset of the launch (k_init skipped; at 16x16x8 most resets
+// overflow the chain anyway), else the items k_init listed.
+template <class CF, bool DIRECT>
 __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
-    const uint32_t cnt = *a.ovf_count;
-    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[1], cnt);
-    for (uint32_t oi = blockIdx.x * INIT_FIX_BLOCK + threadIdx.x; oi < cnt; oi += gridDim.x * INIT_FIX_BLOCK) {
+    const int64_t cnt = DIRECT ? (a.list_count ? (int64_t)*a.list_count : a.n) : (int64_t)*a.ovf_count;
+    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) {
+        if (DIRECT) atomicAdd(&a.stats[0], (uint32_t)cnt);
+        atomicAdd(&a.stats[1], (uint32_t)cnt);
+    }
+    for (int64_t oi = (int64_t)blockIdx.x * INIT_FIX_BLOCK + threadIdx.x; oi < cnt;
+         oi += (int64_t)gridDim.x * INIT_FIX_BLOCK) {
         int64_t b;
         uint32_t seed, slot;
-        init_item(a, (int64_t)a.ovf_list[oi], b, seed, slot);
+        init_item(a, DIRECT ? oi : (int64_t)a.ovf_list[oi], b, seed, slot);
         FullMT mt;
         mt.init(seed, 0u);
         const uint32_t m397 = mt.key[397];  // init_genrand state, before the first twist
+        if (DIRECT && a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;  // else k_init wrote it
         typename CF::Bd P[CF::NP], mask;
 #pragma unroll
         for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
@@ -1713,10 +1721,17 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     if (max_items == 0) return M3_OK;
     int64_t g = (max_items + INIT_BLOCK - 1) / INIT_BLOCK;
     if (g > 4096) g = 4096;
+    if constexpr (CF::N > 128) {  // ~60% of resets overflow the first MT block
+        if (!a.sraw) {            // FullMT for all (no chain stream cache to write)
+            hipLaunchKernelGGL((k_init_fix_lane<CF, true>), dim3((unsigned)g), dim3(INIT_FIX_BLOCK), 0, stream, a);
+            HIP_TRY(hipGetLastError());
+            return M3_OK;
+        }
+    }
     hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
     HIP_TRY(hipGetLastError());
-    if constexpr (CF::N > 128)  // most resets overflow the first MT block: throughput pass
-        hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3(INIT_FIX_GRID), dim3(INIT_FIX_BLOCK), 0, stream, a);
+    if constexpr (CF::N > 128)  // throughput pass
+        hipLaunchKernelGGL((k_init_fix_lane<CF, false>), dim3(INIT_FIX_GRID), dim3(INIT_FIX_BLOCK), 0, stream, a);
     else  // ~1%: latency pass
         hipLaunchKernelGGL(k_init_fix_wave<CF>, dim3(WAVE_FIX_GRID), dim3(64 * WC_WAVES), 0, stream, a);
     HIP_TRY(hipGetLastError());

@@ -156,18 +156,29 @@ def test_c3_1m_boards_properties():
     env.close()
 
 
-def test_autoreset_matches_fresh_episodes():
-    """After autoreset, a board continues with seed + stride exactly like a fresh episode."""
+@pytest.mark.parametrize("tag", list(SHAPES))
+def test_autoreset_matches_fresh_episodes(tag):
+    """After autoreset, a board continues with seed + stride exactly like a fresh episode
+    (16x16x8: the prefetch resets run entirely on the FullMT pass)."""
     n = 2048
-    env = BatchedMatch3Env(n, num_moves=5, env_goal=BIG, seed_base=100, autoreset=True, seed_stride=n)
+    env = BatchedMatch3Env(n, *SHAPES[tag], num_moves=5, env_goal=BIG, seed_base=100, autoreset=True, seed_stride=n)
     for _ in range(5):
         env.step()
     assert env.dones().all()
     assert (env.seeds() == np.arange(100 + n, 100 + 2 * n, dtype=np.uint32)).all()
-    fresh_boards, _, fresh_first = _native.Context().init_boards(np.arange(100 + n, 100 + 2 * n, dtype=np.uint32))
+    fresh_boards, _, fresh_first = _native.Context(*SHAPES[tag]).init_boards(np.arange(100 + n, 100 + 2 * n, dtype=np.uint32))
     assert (env.observations() == fresh_boards).all()
     assert (env.next_actions() == fresh_first).all()
     assert (env.moves() == 0).all() and (env.scores() == 0).all()
+    # the second episode steps like a fresh env on those seeds (the reset's per-board RNG state)
+    fresh = BatchedMatch3Env(n, *SHAPES[tag], num_moves=5, env_goal=BIG,
+                             seeds=np.arange(100 + n, 100 + 2 * n, dtype=np.uint32), autoreset=False)
+    for _ in range(4):
+        env.step()
+        fresh.step()
+        assert (env.rewards() == fresh.rewards()).all()
+        assert (env.observations() == fresh.observations()).all()
+    fresh.close()
     env.close()
 
 
