@@ -74,6 +74,11 @@ constexpr int INIT_FIX_BLOCK = 64;
 #endif
 constexpr int WAVE_FIX_GRID = M3_WAVE_FIX_GRID;  // same, one board per wave (9x9: ~1% of resets)
 constexpr int INIT_BLOCK = 64;
+#ifndef M3_INIT_INLINE_FIX
+#define M3_INIT_INLINE_FIX 1
+#endif
+template <class CF>
+constexpr bool INIT_INLINE_FIX = M3_INIT_INLINE_FIX != 0 && CF::N <= 128;
 constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 
 // Per-shape step-kernel geometry: boards (lanes) per workgroup and the
@@ -597,45 +602,6 @@ __device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t
     return true;
 }
 
-// Reset on the register-only MT19937 chain; grid-strided over n (or *list_count).
-template <class CF>
-__global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
-    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
-    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.stats[0], (uint32_t)cnt);
-    __shared__ uint32_t tm_s[CF::BITS * TileGen<CF>::TWMAX * INIT_BLOCK];
-    __shared__ uint32_t pos_s[TileGen<CF>::MAXR * INIT_BLOCK];
-    uint32_t* tm = tm_s + threadIdx.x;
-    uint32_t* pos = pos_s + threadIdx.x;
-#ifdef M3_PHASE_PROF
-    M3_PROF_LDS(INIT_BLOCK)
-    Prof<NoStore> ps;
-    ps.w = prof_s[threadIdx.x >> 6];
-    const bool live = (int64_t)blockIdx.x * INIT_BLOCK < cnt;
-    if (live) ps.begin();
-#else
-    NoStore* const pp = nullptr;
-#endif
-    for (int64_t i = (int64_t)blockIdx.x * INIT_BLOCK + threadIdx.x; i < cnt;
-         i += (int64_t)gridDim.x * INIT_BLOCK) {
-        int64_t b;
-        uint32_t seed, slot;
-        init_item(a, i, b, seed, slot);
-        const uint32_t m397 = mt_state397(seed);
-#ifdef M3_PHASE_PROF
-        const bool ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, &ps);
-#else
-        const bool ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, pp);
-#endif
-        if (!ok) {
-            const uint32_t o = atomicAdd(a.ovf_count, 1u);
-            a.ovf_list[o] = (uint32_t)i;
-        }
-    }
-#ifdef M3_PHASE_PROF
-    if (live) ps.end(1);
-#endif
-}
-
 // ---- wave-cooperative reset for boards whose reset needs >= 624 draws ----
 // One board per wave. The 624-word MT19937 state sits in LDS; the twist runs
 // on all 64 lanes (three dependency phases), and randint(1, T+1) over the
@@ -714,6 +680,41 @@ __device__ __forceinline__ void wave_fill(uint32_t* key, uint8_t* cells, int lan
     wave_sync();
 }
 
+// One reset (item of the launch) by the whole wave; key: 624 words of LDS, cells: N bytes of LDS.
+template <class CF>
+__device__ void wave_reset(const InitArgs& a, int64_t item, uint32_t* key, uint8_t* cells, int lane) {
+    int64_t b;
+    uint32_t seed, slot;
+    init_item(a, item, b, seed, slot);
+    if (lane == 0) {  // init_genrand is a serial recurrence
+        uint32_t x = seed;
+        for (uint32_t p = 0; p < 624u; ++p) {
+            key[p] = x;
+            x = mt_init_next(x, p + 1u);
+        }
+    }
+    wave_sync();
+    const uint32_t m397 = key[397];
+    uint32_t pos = 624u, k = 0u;
+    wave_fill<CF>(key, cells, lane, pos, k, nullptr);                  // boardv2.py:21
+    typename CF::Bd P[CF::NP], mask;
+    planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
+    while (get_match_mask<CF>(P, mask)) {                               // boardv2.py:23-27
+        wave_fill<CF>(key, cells, lane, pos, k, &mask);
+        planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
+    }
+    const int64_t ob = (int64_t)slot * a.sstride + b;
+    if (lane == 0) init_outputs<CF>(a, b, ob, seed, m397, k, P);
+    if (a.board_words) {
+        for (int q = lane; q < (CF::N + 3) / 4; q += 64)
+            a.board_words[ob * ((CF::N + 3) / 4) + q] = reinterpret_cast<const uint32_t*>(cells)[q];
+    } else {
+        int8_t* dst = a.boards + ob * CF::N;
+        for (int x = lane; x < CF::N; x += 64) dst[x] = (int8_t)cells[x];
+    }
+    wave_sync();
+}
+
 constexpr int WC_WAVES = 4;
 
 template <class CF>
@@ -721,42 +722,66 @@ __global__ void __launch_bounds__(64 * WC_WAVES) k_init_fix_wave(InitArgs a) {
     __shared__ uint32_t key_s[WC_WAVES][624];
     __shared__ __attribute__((aligned(16))) uint8_t cell_s[WC_WAVES][(CF::N + 3) / 4 * 4 + 16];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t* key = key_s[wv];
-    uint8_t* cells = cell_s[wv];
     const uint32_t cnt = *a.ovf_count;
     if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[1], cnt);
-    for (uint32_t oi = blockIdx.x * WC_WAVES + wv; oi < cnt; oi += gridDim.x * WC_WAVES) {
-        int64_t b;
-        uint32_t seed, slot;
-        init_item(a, (int64_t)a.ovf_list[oi], b, seed, slot);
-        if (lane == 0) {  // init_genrand is a serial recurrence
-            uint32_t x = seed;
-            for (uint32_t p = 0; p < 624u; ++p) {
-                key[p] = x;
-                x = mt_init_next(x, p + 1u);
+    for (uint32_t oi = blockIdx.x * WC_WAVES + wv; oi < cnt; oi += gridDim.x * WC_WAVES)
+        wave_reset<CF>(a, (int64_t)a.ovf_list[oi], key_s[wv], cell_s[wv], lane);
+}
+
+// Reset on the register-only MT19937 chain; grid-strided over n (or *list_count).
+// A reset that needs >= 624 draws (~0.7 % at 9x9x6) is redone by its own wave
+// right away (wave_reset) when INIT_INLINE_FIX, else listed for k_init_fix_*.
+template <class CF>
+__global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
+    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
+    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.stats[0], (uint32_t)cnt);
+    __shared__ uint32_t tm_s[CF::BITS * TileGen<CF>::TWMAX * INIT_BLOCK];
+    __shared__ uint32_t pos_s[TileGen<CF>::MAXR * INIT_BLOCK];
+    uint32_t* tm = tm_s + threadIdx.x;
+    uint32_t* pos = pos_s + threadIdx.x;
+#ifdef M3_PHASE_PROF
+    M3_PROF_LDS(INIT_BLOCK)
+    Prof<NoStore> ps;
+    ps.w = prof_s[threadIdx.x >> 6];
+    const bool live = (int64_t)blockIdx.x * INIT_BLOCK < cnt;
+    if (live) ps.begin();
+#else
+    NoStore* const pp = nullptr;
+#endif
+    constexpr bool INLINE = INIT_INLINE_FIX<CF>;
+    static_assert(!INLINE || INIT_BLOCK == 64, "the inline fix is one wave's");
+    __shared__ uint32_t key_s[INLINE ? 624 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t cell_s[INLINE ? (CF::N + 3) / 4 * 4 + 16 : 1];
+    for (int64_t base = (int64_t)blockIdx.x * INIT_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        bool ok = true;
+        if (i < cnt) {
+            int64_t b;
+            uint32_t seed, slot;
+            init_item(a, i, b, seed, slot);
+            const uint32_t m397 = mt_state397(seed);
+#ifdef M3_PHASE_PROF
+            ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, &ps);
+#else
+            ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, pp);
+#endif
+        }
+        if constexpr (INLINE) {  // this wave redoes its >= 624-draw resets at once
+            uint64_t bad = __ballot(!ok);
+            if (bad && a.stats && threadIdx.x == 0) atomicAdd(&a.stats[1], (uint32_t)__builtin_popcountll(bad));
+            while (bad) {
+                const int l = __builtin_ctzll(bad);
+                bad &= bad - 1ull;
+                wave_reset<CF>(a, __shfl(i, l), key_s, cell_s, (int)threadIdx.x);
             }
+        } else if (!ok) {
+            const uint32_t o = atomicAdd(a.ovf_count, 1u);
+            a.ovf_list[o] = (uint32_t)i;
         }
-        wave_sync();
-        const uint32_t m397 = key[397];
-        uint32_t pos = 624u, k = 0u;
-        wave_fill<CF>(key, cells, lane, pos, k, nullptr);                  // boardv2.py:21
-        typename CF::Bd P[CF::NP], mask;
-        planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
-        while (get_match_mask<CF>(P, mask)) {                               // boardv2.py:23-27
-            wave_fill<CF>(key, cells, lane, pos, k, &mask);
-            planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
-        }
-        const int64_t ob = (int64_t)slot * a.sstride + b;
-        if (lane == 0) init_outputs<CF>(a, b, ob, seed, m397, k, P);
-        if (a.board_words) {
-            for (int q = lane; q < (CF::N + 3) / 4; q += 64)
-                a.board_words[ob * ((CF::N + 3) / 4) + q] = reinterpret_cast<const uint32_t*>(cells)[q];
-        } else {
-            int8_t* dst = a.boards + ob * CF::N;
-            for (int x = lane; x < CF::N; x += 64) dst[x] = (int8_t)cells[x];
-        }
-        wave_sync();
     }
+#ifdef M3_PHASE_PROF
+    if (live) ps.end(1);
+#endif
 }
 
 // ---- lane-per-board reset for boards that need >= 624 draws -------------
@@ -1732,7 +1757,7 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     HIP_TRY(hipGetLastError());
     if constexpr (CF::N > 128)  // throughput pass
         hipLaunchKernelGGL((k_init_fix_lane<CF, false>), dim3(INIT_FIX_GRID), dim3(INIT_FIX_BLOCK), 0, stream, a);
-    else  // ~1%: latency pass
+    else if constexpr (!INIT_INLINE_FIX<CF>)  // ~1%: latency pass
         hipLaunchKernelGGL(k_init_fix_wave<CF>, dim3(WAVE_FIX_GRID), dim3(64 * WC_WAVES), 0, stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
