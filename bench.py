@@ -174,8 +174,15 @@ def main():
     rows, cols, types = (int(x) for x in args.shape.split("x"))
 
     # no-op when libm3.so is up to date with its sources and compile flags (build/flags.stamp);
-    # A/B variants are separate files (make variant), selected with M3_LIB
-    subprocess.run(["make", "-s", "-C", PKG], check=True)
+    # A/B variants are separate files (make variant), selected with M3_LIB. The ranks of
+    # one node share the tree: they take turns under a file lock, so at most one builds.
+    import fcntl
+
+    os.makedirs(os.path.join(PKG, "build"), exist_ok=True)
+    with open(os.path.join(PKG, "build", ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", PKG], check=True)
+        fcntl.flock(lk, fcntl.LOCK_UN)
     from match3tile.batched import BatchedMatch3Env
     from match3tile.distributed import seed_plan, timed_steps
 

@@ -87,6 +87,11 @@ struct Cfg {
 // CachedRNG): RAWN raw outputs (RawT holds every mask a step applies: tiles
 // 2^BITS-1, shuffle <= 15, random action < 2^ceil(log2 A)), TSW words of tile
 // stream per plane, ACCW words of acceptance bitmap.
+// boards of at least this many words take the word-sliced legal_masks (0: never)
+#ifndef M3_LEGAL_SLICED_W
+#define M3_LEGAL_SLICED_W 5
+#endif
+
 template <class CF>
 struct StreamCache {
     static constexpr int RAWN = CF::N > 128 ? 512 : 320;
@@ -162,6 +167,85 @@ M3_HD uint32_t extract_bits(const BB<W>& b) {
 // legal_actions (boardFunctions.py:26-112), all 2*R*(C-1) candidates at once.
 // HL bit x: horizontal swap (x, x+1) is legal; VL bit x: vertical swap (x, x+C).
 // --------------------------------------------------------------------------
+// Word-sliced form of the same predicate for wide boards (16x16: W = 8).
+// Every shifted equality at<S>(tb_eq<D>) is rewritten as one comparison of
+// two offsets, [TB[y+S] == TB[y+S+D]], and evaluated one output word at a
+// time straight from the tile planes, so only a few words are live at once:
+// the whole-board form holds ~13 equality boards (104 VGPRs at W = 8) next
+// to the planes and spilled to scratch. Where a shifted offset leaves the
+// board the two forms differ (zero fill of the board vs of the comparison),
+// but every such cell is cleared by the row/column mask its term carries.
+template <int K, int W>
+M3_HD uint32_t wget(const BB<W>& a) {
+    if constexpr (K >= 0 && K < W) return a.w[K];
+    else return 0u;
+}
+// word I of at<D>(a)
+template <int D, int I, int W>
+M3_HD uint32_t wat(const BB<W>& a) {
+    if constexpr (D == 0) {
+        return wget<I>(a);
+    } else if constexpr (D > 0) {
+        constexpr int q = D / 32, s = D % 32;
+        if constexpr (s == 0) return wget<I + q>(a);
+        else return (wget<I + q>(a) >> s) | (wget<I + q + 1>(a) << (32 - s));
+    } else {
+        constexpr int q = (-D) / 32, s = (-D) % 32;
+        if constexpr (s == 0) return wget<I - q>(a);
+        else return (wget<I - q>(a) << s) | (wget<I - q - 1>(a) >> (32 - s));
+    }
+}
+// word I of [TB[y+A] == TB[y+B]]
+template <class CF, int A, int B, int I>
+M3_HD uint32_t weq(const typename CF::Bd* P) {
+    uint32_t r = 0u;
+#pragma unroll
+    for (int p = 0; p < CF::BITS; ++p) r |= wat<A, I>(P[p]) ^ wat<B, I>(P[p]);
+    return ~r;
+}
+template <class CF, int I>
+M3_HD void legal_word(const typename CF::Bd* P, const typename CF::Bd& z0, const typename CF::Bd& spec,
+                      typename CF::Bd& HL, typename CF::Bd& VL) {
+    using G = typename CF::G;
+    constexpr int C = CF::C, R = CF::R;
+    constexpr uint32_t RGE1 = G::row_ge(1).w[I], RGE2 = G::row_ge(2).w[I];
+    constexpr uint32_t RLE2 = G::row_le(R - 2).w[I], RLE3 = G::row_le(R - 3).w[I], RLE4 = G::row_le(R - 4).w[I];
+    constexpr uint32_t CGE1 = G::col_ge(1).w[I], CGE2 = G::col_ge(2).w[I];
+    constexpr uint32_t CLE2 = G::col_le(C - 2).w[I], CLE3 = G::col_le(C - 3).w[I], CLE4 = G::col_le(C - 4).w[I];
+    {   // horizontal (see legal_masks)
+        const uint32_t spc = z0.w[I] | wat<1, I>(z0) | (spec.w[I] & wat<1, I>(spec));
+        const uint32_t condA = CGE2 & weq<CF, -2, 1, I>(P) & weq<CF, -1, 1, I>(P);
+        const uint32_t condB = CLE4 & weq<CF, 0, 2, I>(P) & weq<CF, 0, 3, I>(P);
+        const uint32_t up = RGE1 & weq<CF, -C, 1, I>(P), dn = RLE2 & weq<CF, 1, C, I>(P);
+        const uint32_t up2 = RGE2 & weq<CF, -2 * C, 1, I>(P), dn2 = RLE3 & weq<CF, 1, 2 * C, I>(P);
+        const uint32_t ab1 = (up & dn) | (up & ~dn & up2) | (dn & ~up & dn2);
+        const uint32_t upb = RGE1 & weq<CF, 1 - C, 0, I>(P), dnb = RLE2 & weq<CF, 0, C + 1, I>(P);
+        const uint32_t up2b = RGE2 & weq<CF, 1 - 2 * C, 0, I>(P), dn2b = RLE3 & weq<CF, 0, 2 * C + 1, I>(P);
+        const uint32_t ab2 = (upb & dnb) | (upb & ~dnb & up2b) | (dnb & ~upb & dn2b);
+        HL.w[I] = CLE2 & (spc | ((condA | condB | ab1 | ab2) & ~weq<CF, 0, 1, I>(P)));
+    }
+    {   // vertical
+        const uint32_t spc = z0.w[I] | wat<C, I>(z0) | (spec.w[I] & wat<C, I>(spec));
+        const uint32_t condA = RLE4 & weq<CF, 0, 2 * C, I>(P) & weq<CF, 0, 3 * C, I>(P);
+        const uint32_t condB = RGE2 & weq<CF, -2 * C, C, I>(P) & weq<CF, -C, C, I>(P);
+        const uint32_t l1 = CGE1 & weq<CF, 0, C - 1, I>(P), r1 = CLE2 & weq<CF, 0, C + 1, I>(P);
+        const uint32_t l2 = CGE2 & weq<CF, 0, C - 2, I>(P), r2 = CLE3 & weq<CF, 0, C + 2, I>(P);
+        const uint32_t lr1 = (l1 & r1) | (l1 & ~r1 & l2) | (r1 & ~l1 & r2);
+        const uint32_t l1b = CGE1 & weq<CF, -1, C, I>(P), r1b = CLE2 & weq<CF, 1, C, I>(P);
+        const uint32_t l2b = CGE2 & weq<CF, -2, C, I>(P), r2b = CLE3 & weq<CF, 2, C, I>(P);
+        const uint32_t lr2 = (l1b & r1b) | (l1b & ~r1b & l2b) | (r1b & ~l1b & r2b);
+        VL.w[I] = RLE2 & (spc | ((condA | condB | lr1 | lr2) & ~weq<CF, 0, C, I>(P)));
+    }
+}
+template <class CF, int I = 0>
+M3_HD void legal_words(const typename CF::Bd* P, const typename CF::Bd& z0, const typename CF::Bd& spec,
+                       typename CF::Bd& HL, typename CF::Bd& VL) {
+    if constexpr (I < CF::W) {
+        legal_word<CF, I>(P, z0, spec, HL, VL);
+        legal_words<CF, I + 1>(P, z0, spec, HL, VL);
+    }
+}
+
 template <class CF>
 M3_HD void legal_masks(const typename CF::Bd* P, const typename CF::Bd& spec,
                        typename CF::Bd& HL, typename CF::Bd& VL) {
@@ -170,6 +254,10 @@ M3_HD void legal_masks(const typename CF::Bd* P, const typename CF::Bd& spec,
     constexpr int C = CF::C, R = CF::R;
     constexpr Bd VALID = G::valid();
     const Bd z0 = VALID.andnot(tb_nonzero<CF>(P));  // TB == 0
+    if constexpr (M3_LEGAL_SLICED_W > 0 && CF::W >= M3_LEGAL_SLICED_W) {
+        legal_words<CF>(P, z0, spec, HL, VL);
+        return;
+    }
 
     // equalities shared by both directions
     const Bd e1 = tb_eq<CF, 1>(P), e2 = tb_eq<CF, 2>(P), e3 = tb_eq<CF, 3>(P);
