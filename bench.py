@@ -259,8 +259,9 @@ def main():
         "roofline": {
             "bound": "hbm",
             # one shard's step pipeline: k_env_step + k_env_cont (the continuation of the
-            # long cascades), bracketed by HIP events on the shard's stream
-            "kernel": "k_env_step + k_env_cont",
+            # long cascades) + k_env_fix (dead boards, recomputes), bracketed by HIP events
+            # on the shard's stream
+            "kernel": "k_env_step + k_env_cont + k_env_fix",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

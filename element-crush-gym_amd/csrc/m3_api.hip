@@ -1894,12 +1894,12 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
             HIP_TRY(hipGetLastError());
         }
     }
-    if (timed) {  // the step pipeline of the shard, fixup pass excluded
+    hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    if (timed) {  // the whole step pipeline of the shard, fixup pass included
         HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], st));
         e->tn++;
     }
-    hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
-    HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sh.ev, st));
     if (e->upload_this) {  // the upload two steps ahead rewrites actions[pb] once this shard has read it
         HIP_TRY(hipEventRecord(sh.aev[pb], st));

@@ -40,22 +40,27 @@ static int step_one(typename CF::Bd* P, const int8_t* board, uint32_t seed, int 
     if (pause < 0) {
         r = apply_action<CF>(P, na, act, rng, f, HL, VL, st);
     } else {
-        if (apply_begin<CF>(P, na, act, rng, f, HL, VL, st, r) &&
-            !apply_cascade<CF>(P, rng, f, HL, VL, st, r, pause)) {
-            using K = Cont<CF, Chain>;
-            uint32_t rec[K::WORDS];
-            K::save(P, rng, r, f, [&](int i, uint32_t w) { rec[i] = w; });
-            typename CF::Bd Q[CF::NP];
-            Chain g2;
-            int r2;
-            uint32_t f2;
-            K::load(Q, g2, r2, f2, [&](int i) { return rec[i]; });
-            apply_cascade<CF>(Q, g2, f2, HL, VL, st, r2, -1);
-            memcpy(P, Q, sizeof(Q));
-            rng = g2;
-            r = r2;
-            f = f2;
-            if (paused) ++*paused;
+        // as the env kernels run it: k_env_step stops after `pause` iterations or at a
+        // dead board (before the row shuffle) and hands the state over through the
+        // Cont words; k_env_cont finishes the cascade, dead boards from the shuffle on
+        if (apply_begin<CF>(P, na, act, rng, f, HL, VL, st, r)) {
+            const int c = apply_cascade_ex<CF, CASX_STOP_DEAD>(P, rng, f, HL, VL, st, r, pause, false);
+            if ((c == CAS_PAUSED || c == CAS_DEAD) && !(f & FLAG_RECOMPUTE)) {
+                using K = Cont<CF, Chain>;
+                uint32_t rec[K::WORDS];
+                K::save(P, rng, r, f, [&](int i, uint32_t w) { rec[i] = w; });
+                typename CF::Bd Q[CF::NP];
+                Chain g2;
+                int r2;
+                uint32_t f2;
+                K::load(Q, g2, r2, f2, [&](int i) { return rec[i]; });
+                apply_cascade_ex<CF, 0>(Q, g2, f2, HL, VL, st, r2, -1, c == CAS_DEAD);
+                memcpy(P, Q, sizeof(Q));
+                rng = g2;
+                r = r2;
+                f = f2;
+                if (paused) ++*paused;
+            }
         }
         if (f & FLAG_RECOMPUTE) r = 0;
     }

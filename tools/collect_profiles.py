@@ -6,7 +6,7 @@
 Writes profiles/<round-tag>_bench.json (the bench line), <round-tag>_kernel_stats.csv
 (rocprofv3 --kernel-trace --stats of the same bench command), <round-tag>_pmc.txt
 (per-kernel PMC means, one rocprofv3 pass per counter group) and traffic.json:
-HBM bytes per launch of one shard's step pipeline (k_env_step + k_env_cont, the
+HBM bytes per launch of one shard's step pipeline (k_env_step + k_env_cont + k_env_fix, the
 two kernels bench.py's HIP events bracket) = 2 * FETCH_SIZE + WRITE_SIZE (KB ->
 bytes), the factor 2 being MI355X_MICROARCH.md's gfx950 correction for wide
 coalesced reads (FETCH_SIZE reports half of them; narrower accesses are
@@ -54,7 +54,7 @@ def per_launch(counter):  # mean per launch of each pipeline kernel, summed over
 fetch = per_launch("FETCH_SIZE") * 1024
 write = per_launch("WRITE_SIZE") * 1024
 cfg = bench["config"]
-traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"], "kernel": "k_env_step + k_env_cont",
+traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"], "kernel": "k_env_step + k_env_cont + k_env_fix",
            "boards_per_launch": bench["roofline"].get("boards_per_launch"),
            "fetch_size_bytes": fetch, "write_size_bytes": write,
            "hbm_bytes_per_launch": 2 * fetch + write,
