@@ -38,7 +38,7 @@ pmc = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.p
                      capture_output=True, text=True, check=True).stdout
 open(os.path.join(P, f"{tag}_pmc.txt"), "w").write(pmc)
 
-PIPE = ("k_env_step", "k_env_cont")
+PIPE = ("k_env_step", "k_env_cont", "k_env_fix")
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{src}/**/*_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
