@@ -35,11 +35,27 @@ def algorithmic_bytes_per_step(rows, cols):
     return 2 * rows * cols + 21
 
 
+def host_cores():
+    """(usable cores, nproc, cgroup CPU quota): every core this process may run on -- its affinity
+    set, capped by the cgroup's cpu.max quota when one is set (a GPU box's share of the host)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return (aff if quota is None else min(aff, quota)), os.cpu_count(), quota
+
+
 def cpu_baseline(rows, cols, types, moves, goal, seconds):
-    """The C oracle (bit-exact port of the reference step) on this host's cores, bounded sample."""
+    """The C oracle (bit-exact port of the reference step) on ALL usable host cores, bounded sample,
+    plus the calibrated reference-Python equivalent (profiles/cpu_calibration.json)."""
     from oracle import Oracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, nproc, quota = host_cores()
     o = Oracle(rows, cols, types)
     probe = 2048
     t0 = time.perf_counter()
@@ -50,10 +66,23 @@ def cpu_baseline(rows, cols, types, moves, goal, seconds):
     t0 = time.perf_counter()
     steps, _ = o.run_episodes(seeds, moves, goal, threads)
     dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} seeded {rows}x{cols}x{types} random-action episodes of {moves} moves "
-                      f"(init + legal_actions + choice + apply_action per move; {steps} steps, {dt:.1f} s), "
-                      "oracle/m3_oracle.c, OpenMP over episodes"}
+    res = {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "nproc": nproc, "cgroup_cpus": quota,
+           "kind": "port",
+           "sample": f"{n} seeded {rows}x{cols}x{types} random-action episodes of {moves} moves "
+                     f"(init + legal_actions + choice + apply_action per move; {steps} steps, {dt:.1f} s), "
+                     f"oracle/m3_oracle.c, OpenMP over episodes on {threads} threads"}
+    try:  # C port here / reference Python here, both measured in the build container (tools/calibrate_cpu.py)
+        with open(os.path.join(ROOT, "profiles", "cpu_calibration.json")) as f:
+            cal = json.load(f)
+        if (rows, cols, types) == (9, 9, 6):
+            res["reference_python_equiv"] = {
+                "value": res["value"] * cal["ratio_1core"], "unit": "env-steps/s",
+                "how": "this host's C-port rate x (reference Python / C port per core, both timed on "
+                       f"{cal['cores']} build-container cores: {cal['ref_python_1']['env_steps_per_s']:.0f} / "
+                       f"{cal['c_port_1']['env_steps_per_s']:.0f} env-steps/s), profiles/cpu_calibration.json"}
+    except (OSError, KeyError, ValueError):
+        pass
+    return res
 
 
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
@@ -73,6 +102,92 @@ def load_profile(shape_tag, boards, boards_per_launch):
     except Exception:
         pass
     return {}
+
+
+def dist_setup(world):
+    """Host-side rendezvous of the ranks (torch.distributed over gloo: barriers, the max over ranks,
+    the ncclUniqueId broadcast); RCCL carries the data. None for one process."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    return dist
+
+
+def share_unique_id(dist, rank, make_id):
+    """Rank 0 makes the 128-byte ncclUniqueId, every rank receives it."""
+    obj = [make_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def gather_check(env, dist, rank, world):
+    """After timing: one RCCL all-gather of the last step's packed outcome words, checked against
+    every rank's own words (each rank's slice of the gathered buffer must equal what that rank
+    packed locally; compared through a crc exchanged over gloo). True on every rank iff all agree."""
+    import zlib
+
+    import numpy as np
+    import torch
+
+    from match3tile.distributed import pack_outcomes
+
+    n = env.n
+    got = env.gather(to_host=True).reshape(world, n)
+    mine = pack_outcomes(env.rewards(), env.truncateds(), env.dones())
+    crcs = [None] * world
+    dist.all_gather_object(crcs, zlib.crc32(mine.tobytes()))
+    ok = bool((got[rank] == mine).all()) and all(zlib.crc32(np.ascontiguousarray(got[r]).tobytes()) == crcs[r]
+                                                 for r in range(world))
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def state_digest(env):
+    """crc32 of every board's final state (observation, score, moves, seed, pre-drawn action)."""
+    import zlib
+
+    c = 0
+    for a in (env.observations(), env.scores(), env.moves(), env.seeds(), env.next_actions()):
+        c = zlib.crc32(a.tobytes(), c)
+    return f"{c:08x}"
+
+
+def oracle_sample_check(env, shape, moves, goal, seed_base, stride, total_steps, k=256):
+    """After the clock stops: replay k boards spread over the shard through the C oracle (the
+    checker, never the thing timed) from their first episode, through every same-step autoreset,
+    to the step the env stopped at; compare board, score, moves, seed and the pre-drawn action."""
+    import numpy as np
+
+    from oracle import Oracle
+
+    o = Oracle(*shape)
+    n = env.n
+    idx = np.unique(np.linspace(0, n - 1, k).astype(np.int64))
+    obs = env.observations().reshape(n, -1)
+    score, mv, seeds, nxt = env.scores(), env.moves(), env.seeds(), env.next_actions()
+    bad = 0
+    for b in idx:
+        rem, e = total_steps, 0
+        while True:
+            seed = (seed_base + int(b) + e * stride) & 0xFFFFFFFF
+            ep = o.random_episode(seed, moves, goal)
+            if ep["n"] <= rem:
+                rem -= ep["n"]
+                e += 1
+                if rem == 0:  # autoreset in the step that finished the episode
+                    seed = (seed + stride) & 0xFFFFFFFF
+                    want = (o.init_board(seed)[0].reshape(-1), 0, 0, seed, o.random_episode(seed, 1, goal)["actions"][0])
+                    break
+            else:
+                part = o.random_episode(seed, rem, goal)
+                want = (part["final"].reshape(-1), int(part["rewards"].sum()), rem, seed, ep["actions"][rem])
+                break
+        got = (obs[b], score[b], mv[b], seeds[b], nxt[b])
+        bad += not ((got[0] == want[0]).all() and all(int(x) == int(y) for x, y in zip(got[1:], want[1:])))
+    return {"boards": int(len(idx)), "mismatches": int(bad), "steps_replayed": total_steps}
 
 
 def bench_rollouts(a):
@@ -160,6 +275,11 @@ def main():
                          "5 streams (context + 2 x (step, prefetch)), each on its own hardware queue")
     ap.add_argument("--rollouts", action="store_true",
                     help="secondary bench: device MCTS rollouts (f3) instead of the env step")
+    ap.add_argument("--dry-rendezvous", action="store_true",
+                    help="test hook: run the N>1 rendezvous and unique-id broadcast with a stand-in id, print "
+                         "what each rank received and exit before any GPU work (tests/test_bench_cpu.py)")
+    ap.add_argument("--check-boards", type=int, default=256,
+                    help="boards per rank replayed through the C oracle after the clock stops (0: none)")
     args = ap.parse_args()
     if args.hw_queues is not None:
         if not 1 <= args.hw_queues <= 32:
@@ -173,34 +293,45 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     rows, cols, types = (int(x) for x in args.shape.split("x"))
 
-    # no-op when libm3.so is up to date with its sources and compile flags (build/flags.stamp);
-    # A/B variants are separate files (make variant), selected with M3_LIB. The ranks of
-    # one node share the tree: they take turns under a file lock, so at most one builds.
-    import fcntl
+    dist = dist_setup(world)
+    if args.dry_rendezvous:
+        import hashlib
 
-    os.makedirs(os.path.join(PKG, "build"), exist_ok=True)
-    with open(os.path.join(PKG, "build", ".make.lock"), "w") as lk:
-        fcntl.flock(lk, fcntl.LOCK_EX)
-        subprocess.run(["make", "-s", "-C", PKG], check=True)
-        fcntl.flock(lk, fcntl.LOCK_UN)
+        uid = share_unique_id(dist, rank, lambda: os.urandom(128)) if dist else os.urandom(128)
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local,
+                          "dist_world": dist.get_world_size() if dist else 1,
+                          "id_bytes": len(uid), "id_sha256": hashlib.sha256(uid).hexdigest()}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    # no-op when libm3.so is up to date with its sources and compile flags (build/flags.stamp);
+    # A/B variants are separate files (make variant), selected with M3_LIB (then nothing is
+    # built). The ranks of one node share the tree: they take turns under a file lock, so at
+    # most one builds; a failed build falls back to the library already there.
+    if "M3_LIB" not in os.environ:
+        import fcntl
+
+        os.makedirs(os.path.join(PKG, "build"), exist_ok=True)
+        with open(os.path.join(PKG, "build", ".make.lock"), "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            r = subprocess.run(["make", "-s", "-C", PKG])
+            fcntl.flock(lk, fcntl.LOCK_UN)
+        if r.returncode != 0:
+            if not os.path.exists(os.path.join(PKG, "build", "libm3.so")):
+                raise SystemExit("building libm3.so failed and there is no prebuilt library")
+            print("bench.py: make failed; using the existing build/libm3.so", file=sys.stderr)
     from match3tile.batched import BatchedMatch3Env
     from match3tile.distributed import seed_plan, timed_steps
 
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # host-side rendezvous / barrier / max only (gloo)
-
-        dist.init_process_group("gloo")
-
+    uid = share_unique_id(dist, rank, BatchedMatch3Env.comm_unique_id) if dist else None
     B = args.boards
     seed_base, seed_stride = seed_plan(rank, world, B)
     env = BatchedMatch3Env(B, rows, cols, types, num_moves=args.moves, env_goal=args.goal, device=local,
                            seed_base=seed_base, autoreset=not args.no_autoreset, seed_stride=seed_stride,
                            shards=args.shards)
-    if world > 1:
-        obj = [env.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        env.init_comm(obj[0], world, rank)
+    if dist:
+        env.init_comm(uid, world, rank)
 
     def step():
         env.step()
@@ -211,6 +342,25 @@ def main():
                           on_start=lambda: env.enable_timing(args.steps))
     kms = env.kernel_ms()
     stats = env.stats()
+    # ---- after the clock: attest the run (nothing below is timed) ----
+    nranks = env.comm_size()
+    gather_ok = gather_check(env, dist, rank, world) if dist else None
+    parity = {"digest": state_digest(env)}
+    if dist:
+        digests = [None] * world
+        dist.all_gather_object(digests, parity["digest"])
+        parity["digest_all_ranks"] = digests
+    if args.check_boards and not args.no_autoreset:
+        chk = oracle_sample_check(env, (rows, cols, types), args.moves, args.goal, seed_base, seed_stride,
+                                  args.warmup + args.steps, args.check_boards)
+        if dist:
+            import torch
+
+            t = torch.tensor([chk["boards"], chk["mismatches"]], dtype=torch.int64)
+            dist.all_reduce(t)
+            chk.update(boards=int(t[0]), mismatches=int(t[1]), ranks=world)
+        parity["oracle_sample"] = chk
+        parity["oracle_match"] = chk["mismatches"] == 0
     env.close()
 
     if rank != 0:
@@ -254,6 +404,9 @@ def main():
             "hw_queues": args.hw_queues,
             "autoreset": not args.no_autoreset,
         },
+        "nranks": nranks,
+        "gather_ok": gather_ok,
+        "parity": parity,
         "path_stats": {"autoresets": stats["autoresets"], "reset_recomputes": stats["reset_recomputes"],
                        "step_recomputes": stats["step_recomputes"]},
         "roofline": {

@@ -67,18 +67,12 @@ int set_err(int code, const char* fmt, ...) {
 constexpr int BLOCK = 256;
 constexpr int FIX_BLOCK = 64;
 constexpr int FIX_GRID = 16;       // step fixup almost never has work: few blocks schedule fast
-constexpr int INIT_FIX_GRID = 256;   // resets needing >= 624 draws, one board per lane (16x16)
 constexpr int INIT_FIX_BLOCK = 64;
-#ifndef M3_WAVE_FIX_GRID
-#define M3_WAVE_FIX_GRID 64
-#endif
-constexpr int WAVE_FIX_GRID = M3_WAVE_FIX_GRID;  // same, one board per wave (9x9: ~1% of resets)
 constexpr int INIT_BLOCK = 64;
-#ifndef M3_INIT_INLINE_FIX
-#define M3_INIT_INLINE_FIX 1
-#endif
+// 9x9: k_init redoes its few >= 624-draw resets in-wave (wave_reset); 16x16
+// resets go straight to k_init_fix_lane (most need >= 624 draws)
 template <class CF>
-constexpr bool INIT_INLINE_FIX = M3_INIT_INLINE_FIX != 0 && CF::N <= 128;
+constexpr bool INIT_INLINE_FIX = CF::N <= 128;
 constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 
 // Per-shape step-kernel geometry: boards (lanes) per workgroup and the
@@ -108,27 +102,17 @@ struct KS {
 #endif
     static constexpr int CONT_WPS = CF::N > 128 ? 1 : M3_CONT_WPS;
     static constexpr uint32_t SPILL_RECORDS = 4096;  // spill pool records per shard
-    // per-board stream cache of the batched env (m3_rules.hpp, StreamCache)
-    using SC = StreamCache<CF>;
-    static constexpr int RAWN = SC::RAWN, ACCW = SC::ACCW, TSW = SC::TSW;
-    using RawT = typename SC::RawT;
-    static constexpr int TS_WORDS = CF::BITS * TSW;                 // per board in HBM
-    static constexpr int LDS_WORDS = CF::BITS * (TSW + 1) + ACCW;   // per lane in LDS (+ zero pad per plane)
-#ifndef M3_ENV_CHAIN
-#define M3_ENV_CHAIN 1
-#endif
-    // The env step's RNG: CHAIN = the register-only MT19937 chain from the
-    // board's (seed, mt[397]) -- 4 B of per-board state; otherwise the
-    // per-board stream cache (RAWN raw outputs + tile planes, ~420 B read per
-    // step at 9x9), built by the reset.
-    static constexpr bool CHAIN = M3_ENV_CHAIN != 0;
+    // The env step's RNG is the register-only MT19937 chain from the board's
+    // (seed, mt[397]) -- 4 B of per-board state (a per-board stream cache of
+    // the first raw outputs, built by the reset, measured equal at 9x9 and 2x
+    // slower at 16x16; removed in round 3).
     // 16x16: one chain level (draws < 227; a step needing more -- a near-full
     // board refill -- goes to k_env_fix), five fewer VGPRs live through the
     // cascade, +2.5 %. 9x9: the full three-level chain; the one-level build
     // came out 16 % slower (A/B gpurun_out/ab3), the register allocation of
     // the 3-waves/SIMD bound shifts with it.
     using Chain = std::conditional_t<(CF::N > 128), ChainMT1, ChainMT>;
-    using Rng = std::conditional_t<CHAIN, Chain, typename SC::Rng>;
+    using Rng = Chain;
 #ifndef M3_CASCADE_LIMIT
 #define M3_CASCADE_LIMIT 2
 #endif
@@ -140,11 +124,6 @@ struct KS {
 #define M3_CASCADE_LIMIT16 -1
 #endif
     static constexpr int CASCADE_LIMIT = CF::N > 128 ? M3_CASCADE_LIMIT16 : M3_CASCADE_LIMIT;
-#ifndef M3_ENV_WF
-#define M3_ENV_WF 0
-#endif
-    // the env step as the multi-kernel pipeline k_wf_* (else k_env_step + k_env_cont)
-    static constexpr bool WAVEFRONT = M3_ENV_WF != 0;
 };
 
 // Per-lane match-group table (see m3_rules.hpp, match_scan): the first CAP
@@ -494,15 +473,7 @@ struct InitArgs {
     uint8_t* done;
     uint8_t* trunc;
     uint32_t* flags;
-    uint32_t* ovf_count;         // items whose reset needed >= 624 draws (k_init_fix)
-    uint32_t* ovf_list;          // item indices
-    uint32_t* stats;             // nullable: [0] resets, [1] reset recomputes
-    // nullable: stream cache of slot s, board b: raw row (s*cstride + b)*RAWN,
-    // tile word (p, w) at s*TS_WORDS*cstride + (p*TSW + w)*cstride + b,
-    // acceptance word w at s*ACCW*cstride + w*cstride + b
-    void* sraw;
-    uint32_t* sts;
-    uint32_t* sacc;
+    uint32_t* stats;             // nullable: [0] resets, [1] reset recomputes (>= 624 draws)
     uint32_t* m397;              // nullable: mt[397] of the seed's init_genrand state at (slot, b)
     int64_t cstride;
 };
@@ -556,42 +527,18 @@ __device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, int64
     if (a.flags) a.flags[b] = fa < 0 ? FLAG_NO_LEGAL : 0u;
 }
 
-// Reset of board b on a tile stream generated in LDS (init_board_tiles); with
-// the env's cache pointers set it also writes the step's stream cache.
-// Returns false if the reset needs >= 624 draws (k_init_fix redoes it).
+// Reset of board b on a tile stream generated in LDS (init_board_tiles).
+// Returns false if the reset needs >= 624 draws (wave_reset / k_init_fix redo it).
 template <class CF, class S = NoStore>
 __device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t slot, uint32_t m397,
                                           uint32_t* tm, uint32_t* pos, S* ps = nullptr) {
-    using K = KS<CF>;
-    using RawT = typename K::RawT;
-    constexpr int TW = TileGen<CF>::TWMAX;
     typename CF::Bd P[CF::NP];
     ChainMT g;
     g.init(seed, m397);
-    const int64_t cb = (int64_t)slot * a.cstride + b;  // cache row of (slot, b)
-    if (a.m397) a.m397[cb] = m397;
-    RawT* row = a.sraw ? static_cast<RawT*>(a.sraw) + cb * K::RAWN : nullptr;
-    uint32_t* sacc = a.sacc ? a.sacc + (int64_t)slot * K::ACCW * a.cstride + b : nullptr;
-    uint32_t* sts = a.sts ? a.sts + (int64_t)slot * K::TS_WORDS * a.cstride + b : nullptr;
+    if (a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;
     uint32_t draws = 0;
-    constexpr uint32_t PER = 4u / sizeof(RawT), SH = 8u * sizeof(RawT);
-    uint32_t pk = 0u;  // PER raw entries per dword store (k is the same on every lane)
     const bool ok = init_board_tiles<CF>(
-        P, g, tm, pos, INIT_BLOCK, draws, a.sraw ? (uint32_t)K::RAWN : 0u,
-        [&](uint32_t k, uint32_t v) {
-            pk |= (v & ((1u << SH) - 1u)) << (SH * (k % PER));
-            if (k % PER == PER - 1u) {
-                reinterpret_cast<uint32_t*>(row)[k / PER] = pk;
-                pk = 0u;
-            }
-        },
-        [&](uint32_t w, uint32_t v) { sacc[(int64_t)w * a.cstride] = v; }, ps);
-    if (sts) {
-#pragma unroll
-        for (int p = 0; p < CF::BITS; ++p)
-#pragma unroll
-            for (int w = 0; w < K::TSW; ++w) sts[(int64_t)(p * K::TSW + w) * a.cstride] = tm[(p * TW + w) * INIT_BLOCK];
-    }
+        P, g, tm, pos, INIT_BLOCK, draws, 0u, [](uint32_t, uint32_t) {}, [](uint32_t, uint32_t) {}, ps);
     if (!ok) return false;
     const int64_t ob = (int64_t)slot * a.sstride + b;
     init_outputs<CF>(a, b, ob, seed, m397, draws, P);
@@ -715,22 +662,9 @@ __device__ void wave_reset(const InitArgs& a, int64_t item, uint32_t* key, uint8
     wave_sync();
 }
 
-constexpr int WC_WAVES = 4;
-
-template <class CF>
-__global__ void __launch_bounds__(64 * WC_WAVES) k_init_fix_wave(InitArgs a) {
-    __shared__ uint32_t key_s[WC_WAVES][624];
-    __shared__ __attribute__((aligned(16))) uint8_t cell_s[WC_WAVES][(CF::N + 3) / 4 * 4 + 16];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t cnt = *a.ovf_count;
-    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[1], cnt);
-    for (uint32_t oi = blockIdx.x * WC_WAVES + wv; oi < cnt; oi += gridDim.x * WC_WAVES)
-        wave_reset<CF>(a, (int64_t)a.ovf_list[oi], key_s[wv], cell_s[wv], lane);
-}
-
 // Reset on the register-only MT19937 chain; grid-strided over n (or *list_count).
 // A reset that needs >= 624 draws (~0.7 % at 9x9x6) is redone by its own wave
-// right away (wave_reset) when INIT_INLINE_FIX, else listed for k_init_fix_*.
+// right away (wave_reset).
 template <class CF>
 __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
@@ -748,10 +682,9 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
 #else
     NoStore* const pp = nullptr;
 #endif
-    constexpr bool INLINE = INIT_INLINE_FIX<CF>;
-    static_assert(!INLINE || INIT_BLOCK == 64, "the inline fix is one wave's");
-    __shared__ uint32_t key_s[INLINE ? 624 : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t cell_s[INLINE ? (CF::N + 3) / 4 * 4 + 16 : 1];
+    static_assert(INIT_INLINE_FIX<CF> && INIT_BLOCK == 64, "the in-wave redo is one wave's");
+    __shared__ uint32_t key_s[624];
+    __shared__ __attribute__((aligned(16))) uint8_t cell_s[(CF::N + 3) / 4 * 4 + 16];
     for (int64_t base = (int64_t)blockIdx.x * INIT_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_BLOCK) {
         const int64_t i = base + threadIdx.x;
         bool ok = true;
@@ -766,17 +699,13 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
             ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, pp);
 #endif
         }
-        if constexpr (INLINE) {  // this wave redoes its >= 624-draw resets at once
-            uint64_t bad = __ballot(!ok);
-            if (bad && a.stats && threadIdx.x == 0) atomicAdd(&a.stats[1], (uint32_t)__builtin_popcountll(bad));
-            while (bad) {
-                const int l = __builtin_ctzll(bad);
-                bad &= bad - 1ull;
-                wave_reset<CF>(a, __shfl(i, l), key_s, cell_s, (int)threadIdx.x);
-            }
-        } else if (!ok) {
-            const uint32_t o = atomicAdd(a.ovf_count, 1u);
-            a.ovf_list[o] = (uint32_t)i;
+        // this wave redoes its >= 624-draw resets at once
+        uint64_t bad = __ballot(!ok);
+        if (bad && a.stats && threadIdx.x == 0) atomicAdd(&a.stats[1], (uint32_t)__builtin_popcountll(bad));
+        while (bad) {
+            const int l = __builtin_ctzll(bad);
+            bad &= bad - 1ull;
+            wave_reset<CF>(a, __shfl(i, l), key_s, cell_s, (int)threadIdx.x);
         }
     }
 #ifdef M3_PHASE_PROF
@@ -835,36 +764,48 @@ __device__ __forceinline__ void fill_round(typename CF::Bd* P, RNG& mt, const ty
     }
 }
 
-// DIRECT: every reset of the launch (k_init skipped; at 16x16x8 most resets
-// overflow the chain anyway), else the items k_init listed.
-template <class CF, bool DIRECT>
+// Every reset of the launch (k_init is skipped at 16x16x8: most resets
+// overflow the chain anyway). stats[1] counts the resets that needed >= 624
+// draws, as k_init's in-wave redo does at 9x9, so the counter means the same
+// at both shapes.
+template <class CF>
 __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
-    const int64_t cnt = DIRECT ? (a.list_count ? (int64_t)*a.list_count : a.n) : (int64_t)*a.ovf_count;
-    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) {
-        if (DIRECT) atomicAdd(&a.stats[0], (uint32_t)cnt);
-        atomicAdd(&a.stats[1], (uint32_t)cnt);
-    }
-    for (int64_t oi = (int64_t)blockIdx.x * INIT_FIX_BLOCK + threadIdx.x; oi < cnt;
-         oi += (int64_t)gridDim.x * INIT_FIX_BLOCK) {
-        int64_t b;
-        uint32_t seed, slot;
-        init_item(a, DIRECT ? oi : (int64_t)a.ovf_list[oi], b, seed, slot);
-        FullMT mt;
-        mt.init(seed, 0u);
-        const uint32_t m397 = mt.key[397];  // init_genrand state, before the first twist
-        if (DIRECT && a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;  // else k_init wrote it
-        typename CF::Bd P[CF::NP], mask;
+    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
+    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], (uint32_t)cnt);
+    for (int64_t base = (int64_t)blockIdx.x * INIT_FIX_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_FIX_BLOCK) {
+        const int64_t oi = base + threadIdx.x;
+        bool long_reset = false;
+        if (oi < cnt) {
+            int64_t b;
+            uint32_t seed, slot;
+            init_item(a, oi, b, seed, slot);
+            FullMT mt;
+            mt.init(seed, 0u);
+            const uint32_t m397 = mt.key[397];  // init_genrand state, before the first twist
+            if (a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;
+            typename CF::Bd P[CF::NP], mask;
 #pragma unroll
-        for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
-        fill_round<CF>(P, mt, nullptr);                              // boardv2.py:21
-        while (get_match_mask<CF>(P, mask)) fill_round<CF>(P, mt, &mask);  // boardv2.py:23-27
-        const int64_t ob = (int64_t)slot * a.sstride + b;
-        init_outputs<CF>(a, b, ob, seed, m397, mt.draws(), P);
-        constexpr int NW = (CF::N + 3) / 4;
-        uint32_t cw[NW];
-        words_from_planes<CF>(P, cw);
-        init_store_board<CF>(a, ob, cw);
+            for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+            fill_round<CF>(P, mt, nullptr);                              // boardv2.py:21
+            while (get_match_mask<CF>(P, mask)) fill_round<CF>(P, mt, &mask);  // boardv2.py:23-27
+            const int64_t ob = (int64_t)slot * a.sstride + b;
+            init_outputs<CF>(a, b, ob, seed, m397, mt.draws(), P);
+            constexpr int NW = (CF::N + 3) / 4;
+            uint32_t cw[NW];
+            words_from_planes<CF>(P, cw);
+            init_store_board<CF>(a, ob, cw);
+            long_reset = mt.draws() >= 624u;
+        }
+        const uint64_t m = __ballot(long_reset);
+        if (m && a.stats && (threadIdx.x & 63) == 0) atomicAdd(&a.stats[1], (uint32_t)__popcll(m));
     }
+}
+
+// mt[397] of init_genrand(seeds[b]): the chain word of each board's current
+// episode (env resume, m3_env_set)
+__global__ void __launch_bounds__(256) k_mt397(int64_t n, const uint32_t* seeds, uint32_t* out) {
+    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < n; b += (int64_t)gridDim.x * 256)
+        out[b] = mt_state397(seeds[b]);
 }
 
 template <class CF>
@@ -916,8 +857,7 @@ struct EnvArgs {
     uint32_t* legal;  // nullable
     int32_t* packed;  // nullable: reward<<2 | trunc<<1 | done for the RCCL gather
     uint32_t* counters;  // this step's block: [0] overflow count, [1] prefetch count, [2] prefetch overflow
-                         // count, [3] spill records used, [4] continuation records (k_wf_*: of
-                         // k_wf_begin), [5] [6] of the k_wf_pass passes, [7] dead boards
+                         // count, [3] spill records used, [4] continuation records
     uint32_t* spill;     // group-table spill pool of the shard
     uint32_t* stats;     // [0] step recomputes
     uint32_t* ovf_list;
@@ -928,18 +868,10 @@ struct EnvArgs {
     uint32_t* pf_list;   // prefetch queue of this step: board, seed, slot
     uint32_t* pf_seed;
     uint32_t* pf_slot;
-    const void* sraw;    // stream caches of the NSLOT slots (layout: InitArgs; KS::CHAIN: unused)
-    const uint32_t* sts;
-    const uint32_t* sacc;
-    const uint32_t* m397;  // [NSLOT][cstride] mt[397] of each slot's seed (KS::CHAIN)
+    const uint32_t* m397;  // [NSLOT][cstride] mt[397] of each slot's seed
     int64_t cstride;
     uint32_t* cont;        // nullable: continuation records of paused steps (k_env_cont), [1 + WORDS][cont_stride]
     int64_t cont_stride;
-    // multi-kernel step (k_wf_*): a second record buffer and the settled state
-    // of every board, [EnvCont::WORDS][cont_stride] by board
-    uint32_t* cont2;
-    uint32_t* settled;
-    uint32_t* dead_list;  // boards k_wf_finish found dead (counters[7] of them)
 };
 
 // Match3Env.step bookkeeping (env.py:48-56) after BoardV2.apply_action (r, f,
@@ -1075,27 +1007,11 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
     uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
     uint32_t* const gtab = stage_tab;
-    __shared__ uint32_t cache_s[K::CHAIN ? 1 : K::LDS_WORDS * K::B];
     const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
     const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
     block_copy_in<CF::N, KS<CF>::B>(a.cur + b0 * CF::N, lds, nb);
     const int t = threadIdx.x;
     const uint32_t cslot = t < nb ? a.slot[b0 + t] : 0u;
-    if (!K::CHAIN && t < nb) {  // this lane's tile planes (+ zero pad) and acceptance words, lane-interleaved
-        const int64_t b = b0 + t;
-        const uint32_t* sts = a.sts + (int64_t)cslot * K::TS_WORDS * a.cstride + b;
-        const uint32_t* sacc = a.sacc + (int64_t)cslot * K::ACCW * a.cstride + b;
-#pragma unroll
-        for (int p = 0; p < CF::BITS; ++p) {
-#pragma unroll
-            for (int w = 0; w < K::TSW; ++w)
-                cache_s[(p * (K::TSW + 1) + w) * K::B + t] = sts[(int64_t)(p * K::TSW + w) * a.cstride];
-            cache_s[(p * (K::TSW + 1) + K::TSW) * K::B + t] = 0u;
-        }
-#pragma unroll
-        for (int w = 0; w < K::ACCW; ++w)
-            cache_s[(CF::BITS * (K::TSW + 1) + w) * K::B + t] = sacc[(int64_t)w * a.cstride];
-    }
     __syncthreads();
 #ifdef M3_PHASE_PROF
     M3_PROF_LDS(KS<CF>::B)
@@ -1115,11 +1031,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
         typename CF::Bd P[CF::NP];
         lds_to_planes<CF>(lds, t, P);
         typename K::Rng rng;
-        if constexpr (K::CHAIN)
-            rng.init(a.seeds[b], a.m397[(int64_t)cslot * a.cstride + b]);
-        else
-            rng.init(static_cast<const typename K::RawT*>(a.sraw) + ((int64_t)cslot * a.cstride + b) * K::RAWN,
-                     cache_s + t, cache_s + CF::BITS * (K::TSW + 1) * K::B + t, K::B);
+        rng.init(a.seeds[b], a.m397[(int64_t)cslot * a.cstride + b]);
         int r;
         uint32_t f;
         int res;
@@ -1222,238 +1134,6 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
         uint32_t f;
         env_step_one<CF, false>(P, a, b, mt, st, -1, r, f);
         planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * CF::N));
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Multi-kernel env step ("wavefront"): the same Match3Env.step as k_env_step,
-// cut at the cascade's iteration boundaries so that every launch runs one
-// coherent piece of work on one board per lane, with its live state in HBM
-// between launches (HBM bandwidth is the resource this path has in plenty):
-//   k_wf_begin   all boards, natural order: swap, combos, first match + clear,
-//                first cascade iteration;
-//   k_wf_pass    the boards still matching, compacted: one more iteration
-//                (twice), then the rest of the cascade (tail, ~8 %);
-//   k_wf_finish  all boards, natural order: legal set, next seeded random
-//                action, Match3Env bookkeeping, autoreset swap, board bytes;
-//   k_env_fix    exact recompute of every board flagged on the way (RNG past
-//                the chain, group-table overflow, dead board: the shuffle).
-// Each kernel holds only its own phase's registers (the megakernel peaks at
-// ~220 VGPRs where legal masks, cascade and shuffle meet), so more waves fit a
-// SIMD, and no lane idles through another board's longer cascade.
-// Board b's settled state: settled[w * cont_stride + b], w < EnvCont::WORDS
-// (flags word FW: FLAG_RECOMPUTE set = k_env_fix owns the board this step).
-// ---------------------------------------------------------------------------
-template <class CF>
-struct WF {
-    using K = KS<CF>;
-    using C = EnvCont<CF>;
-    static constexpr int FW = C::WORDS - 1;  // flags word of a settled state
-#ifndef M3_WF_WPS
-#define M3_WF_WPS 4
-#endif
-    static constexpr int WPS = CF::N > 128 ? 1 : M3_WF_WPS;  // waves per SIMD the wf kernels are bounded for
-#ifndef M3_WF_BEGIN_LIMIT
-#define M3_WF_BEGIN_LIMIT 2
-#endif
-#ifndef M3_WF_PASSES
-#define M3_WF_PASSES 0
-#endif
-    static constexpr int BEGIN_LIMIT = M3_WF_BEGIN_LIMIT;  // cascade iterations in k_wf_begin
-    static constexpr int PASSES = M3_WF_PASSES;            // one-iteration k_wf_pass launches before the tail
-    static_assert(BEGIN_LIMIT >= 1 && PASSES >= 0 && PASSES <= 2, "record counters [4 .. 6]");
-};
-
-template <class CF>
-__device__ __forceinline__ void wf_settle(const EnvArgs& a, int64_t b, const typename CF::Bd* P,
-                                          const typename KS<CF>::Rng& rng, int r, uint32_t f) {
-    const int64_t cs = a.cont_stride;
-    EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { a.settled[(int64_t)i * cs + b] = w; });
-}
-
-__device__ __forceinline__ void wf_recompute(const EnvArgs& a, int64_t b, uint32_t f, int fw) {
-    a.settled[(int64_t)fw * a.cont_stride + b] = f | FLAG_RNG_OVERFLOW;  // any FLAG_RECOMPUTE bit
-    const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-    a.ovf_list[slot] = (uint32_t)b;
-}
-
-// ballot-compacted continuation record (one atomic per wave)
-template <class CF>
-__device__ __forceinline__ void wf_push(const EnvArgs& a, uint32_t* out, uint32_t* count, bool want, int64_t b,
-                                        const typename CF::Bd* P, const typename KS<CF>::Rng& rng, int r,
-                                        uint32_t f) {
-    const uint64_t m = __ballot(want);
-    if (!m) return;
-    const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (want) {
-        const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        uint32_t* rec = out + q;
-        const int64_t cs = a.cont_stride;
-        rec[0] = (uint32_t)b;
-        EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
-    }
-}
-
-// swap, combos, first clear and the first cascade iteration of every board
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, WF<CF>::WPS) k_wf_begin(EnvArgs a) {
-    using K = KS<CF>;
-    constexpr int STAGE_WORDS = (K::B * CF::N + 16 + 3) / 4;
-    constexpr int TAB_WORDS = LdsStore<CF, K::GCAP, K::B>::WORDS;
-    // staging (read once, before the table is first written) aliases the group table
-    __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
-    uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
-    const int64_t b0 = (int64_t)blockIdx.x * K::B;
-    const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
-    block_copy_in<CF::N, K::B>(a.cur + b0 * CF::N, lds, nb);
-    __syncthreads();
-    const int t = threadIdx.x;
-    LdsStore<CF, K::GCAP, K::B> st{stage_tab + t};
-    st.spill = a.spill;
-    st.pool_next = &a.counters[3];
-    st.pool_cap = K::SPILL_RECORDS;
-    if (t >= nb) return;
-    const int64_t b = b0 + t;
-    typename CF::Bd P[CF::NP];
-    lds_to_planes<CF>(lds, t, P);
-    const uint32_t cslot = a.slot[b];
-    typename K::Rng rng;
-    rng.init(a.seeds[b], a.m397[(int64_t)cslot * a.cstride + b]);
-    const int act_in = a.actions ? a.actions[b] : a.next_action[b];
-    const int mv = a.moves[b];
-    int r;
-    uint32_t f;
-    typename CF::Bd HL, VL;
-    int cs = CAS_SETTLED;
-    if (apply_begin<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st, r, false))
-        cs = apply_cascade_ex<CF, CASX_STOP_SETTLED>(P, rng, f, HL, VL, st, r, WF<CF>::BEGIN_LIMIT, false);
-    const bool redo = (f & FLAG_RECOMPUTE) != 0;
-    const bool paused = !redo && cs == CAS_PAUSED;
-    if (redo) wf_recompute(a, b, f, WF<CF>::FW);
-    else if (!paused) wf_settle<CF>(a, b, P, rng, r, f);
-    wf_push<CF>(a, a.cont, &a.counters[4], paused, b, P, rng, r, f);
-}
-
-// one more cascade iteration (limit 1) or the rest of it (limit -1) of the
-// records in rin (count *cin); still-matching boards go to rout (*cout)
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, WF<CF>::WPS) k_wf_pass(EnvArgs a, const uint32_t* rin,
-                                                                      const uint32_t* cin, uint32_t* rout,
-                                                                      uint32_t* cout, int limit) {
-    using K = KS<CF>;
-    __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
-    const uint32_t cnt = *cin;
-    LdsStore<CF, K::GCAP, K::B> st{tab + threadIdx.x};
-    st.spill = a.spill;
-    st.pool_next = &a.counters[3];
-    st.pool_cap = K::SPILL_RECORDS;
-    const int64_t cs = a.cont_stride;
-    for (uint32_t q0 = blockIdx.x * K::B; q0 < cnt; q0 += gridDim.x * K::B) {
-        const uint32_t q = q0 + threadIdx.x;
-        const bool live = q < cnt;
-        int64_t b = 0;
-        typename CF::Bd P[CF::NP];
-        typename K::Rng rng;
-        int r = 0;
-        uint32_t f = 0;
-        bool paused = false;
-        if (live) {
-            const uint32_t* rec = rin + q;
-            b = rec[0];
-            EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
-            typename CF::Bd HL, VL;
-            const int c = apply_cascade_ex<CF, CASX_STOP_SETTLED>(P, rng, f, HL, VL, st, r, limit, false);
-            const bool redo = (f & FLAG_RECOMPUTE) != 0;
-            paused = !redo && c == CAS_PAUSED;
-            if (redo) wf_recompute(a, b, f, WF<CF>::FW);
-            else if (!paused) wf_settle<CF>(a, b, P, rng, r, f);
-        }
-        if (rout) wf_push<CF>(a, rout, cout, paused, b, P, rng, r, f);
-    }
-}
-
-// legal set, next seeded random action, bookkeeping, autoreset swap and the
-// board bytes of every board
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, WF<CF>::WPS) k_wf_finish(EnvArgs a) {
-    using K = KS<CF>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[K::B * CF::N + 16];
-    const int64_t b0 = (int64_t)blockIdx.x * K::B;
-    const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
-    const int t = threadIdx.x;
-    if (t < nb) {
-        const int64_t b = b0 + t;
-        const int64_t cs = a.cont_stride;
-        uint32_t f = a.settled[(int64_t)WF<CF>::FW * cs + b];
-        typename CF::Bd P[CF::NP];
-#pragma unroll
-        for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
-        if (!(f & FLAG_RECOMPUTE)) {  // else k_env_fix writes this board
-            typename K::Rng rng;
-            int r;
-            const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
-            if (stepped) {
-                EnvCont<CF>::load(P, rng, r, f, [&](int i) { return a.settled[(int64_t)i * cs + b]; });
-            } else {  // the board is unchanged: its bytes (all 7 planes) are the input
-                bytes_to_planes<CF>(a.cur + b * CF::N, P);
-                rng.init(0u, 0u);
-                r = 0;
-            }
-            const int mv = a.moves[b], sc0 = a.score[b];
-            typename CF::Bd HL, VL;
-            legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
-            NoStore ns;
-            if (stepped && !(HL.any() || VL.any())) {  // dead board: the shuffle path, k_wf_dead
-                const uint32_t slot = atomicAdd(&a.counters[7], 1u);
-                a.dead_list[slot] = (uint32_t)b;
-            } else if (!env_finish<CF>(P, a, b, rng, ns, r, f, HL, VL, mv, sc0)) {
-                const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-                a.ovf_list[slot] = (uint32_t)b;
-            }
-        }
-        planes_to_bytes<CF>(P, lds + t * CF::N);
-    }
-    __syncthreads();
-    block_copy_out<CF::N, K::B>(a.nxt + b0 * CF::N, lds, nb);
-}
-
-// Dead boards (no legal move once settled: ~1e-5 of steps): the row shuffle
-// and whatever follows it (boardv2.py:188-202) from the settled state, on the
-// same register MT chain -- a few lanes, one small grid, instead of the
-// FullMT recompute.
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B) k_wf_dead(EnvArgs a) {
-    using K = KS<CF>;
-    __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
-    const uint32_t cnt = a.counters[7];
-    LdsStore<CF, K::GCAP, K::B> st{tab + threadIdx.x};
-    st.spill = a.spill;
-    st.pool_next = &a.counters[3];
-    st.pool_cap = K::SPILL_RECORDS;
-    const int64_t cs = a.cont_stride;
-    for (uint32_t q = blockIdx.x * K::B + threadIdx.x; q < cnt; q += gridDim.x * K::B) {
-        const int64_t b = a.dead_list[q];
-        typename CF::Bd P[CF::NP];
-        typename K::Rng rng;
-        int r;
-        uint32_t f;
-        EnvCont<CF>::load(P, rng, r, f, [&](int i) { return a.settled[(int64_t)i * cs + b]; });
-        const int mv = a.moves[b], sc0 = a.score[b];
-        typename CF::Bd HL, VL;
-        apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, -1, true);
-        const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0);
-        if (!ok) {
-            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-            a.ovf_list[slot] = (uint32_t)b;
-        } else {
-            constexpr int NW = (CF::N + 3) / 4;
-            uint32_t cw[NW];
-            words_from_planes<CF>(P, cw);
-            store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.nxt + b * CF::N), cw);
-        }
     }
 }
 
@@ -1627,6 +1307,7 @@ struct m3_env {
     int autoreset = 0;
     uint32_t stride = 0;
     bool ready = false;
+    bool stale = false;  // fields were loaded with m3_env_set: rederive() before the next step
     int8_t* boards[2] = {nullptr, nullptr};
     int cur = 0;
     uint32_t *seeds = nullptr, *flags = nullptr, *draws = nullptr, *legal = nullptr;
@@ -1655,15 +1336,10 @@ struct m3_env {
     uint32_t* ne_words = nullptr;
     int32_t* ne_first = nullptr;
     uint32_t* ne_legal = nullptr;
-    void* sraw = nullptr;
-    uint32_t *sts = nullptr, *sacc = nullptr;
     uint32_t* m397 = nullptr;  // [NSLOT][n]
-    uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont, k_wf_*)
-    uint32_t* cont2 = nullptr;    // second record buffer (k_wf_pass)
-    uint32_t* settled = nullptr;  // settled state of every board [EnvCont::WORDS][n] (k_wf_*)
-    uint32_t* dead_list = nullptr;  // [n] (k_wf_dead)
+    uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont)
     // prefetch queues and their overflow lists, by step % PF_LAG
-    uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {}, *pf_ovf[PF_LAG] = {};
+    uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {};
     int64_t steps = 0;
     int32_t* packed = nullptr;
     int32_t* gathered = nullptr;
@@ -1740,25 +1416,15 @@ int launch_apply(m3_ctx* c, const ApplyArgs& a) {
     return M3_OK;
 }
 
-// ovf_count must be zeroed on the stream before this call.
 template <class CF>
 int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     if (max_items == 0) return M3_OK;
     int64_t g = (max_items + INIT_BLOCK - 1) / INIT_BLOCK;
     if (g > 4096) g = 4096;
-    if constexpr (CF::N > 128) {  // ~60% of resets overflow the first MT block
-        if (!a.sraw) {            // FullMT for all (no chain stream cache to write)
-            hipLaunchKernelGGL((k_init_fix_lane<CF, true>), dim3((unsigned)g), dim3(INIT_FIX_BLOCK), 0, stream, a);
-            HIP_TRY(hipGetLastError());
-            return M3_OK;
-        }
-    }
-    hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
-    HIP_TRY(hipGetLastError());
-    if constexpr (CF::N > 128)  // throughput pass
-        hipLaunchKernelGGL((k_init_fix_lane<CF, false>), dim3(INIT_FIX_GRID), dim3(INIT_FIX_BLOCK), 0, stream, a);
-    else if constexpr (!INIT_INLINE_FIX<CF>)  // ~1%: latency pass
-        hipLaunchKernelGGL(k_init_fix_wave<CF>, dim3(WAVE_FIX_GRID), dim3(64 * WC_WAVES), 0, stream, a);
+    if constexpr (INIT_INLINE_FIX<CF>)
+        hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
+    else  // ~60% of 16x16x8 resets overflow the first MT block: FullMT for all
+        hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3((unsigned)g), dim3(INIT_FIX_BLOCK), 0, stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }
@@ -1778,11 +1444,6 @@ void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
     r.board_words = e->ne_words + o * ((CF::N + 3) / 4);
     r.first_action = e->ne_first + o;
     r.legal = e->ne_legal + o * CF::AW;
-    if constexpr (!KS<CF>::CHAIN) {
-        r.sraw = static_cast<typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
-        r.sts = e->sts + o;
-        r.sacc = e->sacc + o;
-    }
     r.m397 = e->m397 + o;
     r.cstride = e->n;
 }
@@ -1842,20 +1503,9 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.pf_list = e->pf_list[par] + o;
     a.pf_seed = e->pf_seed[par] + o;
     a.pf_slot = e->pf_slot[par] + o;
-    if constexpr (!KS<CF>::CHAIN) {
-        a.sraw = static_cast<const typename KS<CF>::RawT*>(e->sraw) + o * KS<CF>::RAWN;
-        a.sts = e->sts + o;
-        a.sacc = e->sacc + o;
-    } else {
-        a.sraw = nullptr;
-        a.sts = a.sacc = nullptr;
-    }
     a.m397 = e->m397 + o;
     a.cstride = e->n;
-    a.cont = (KS<CF>::WAVEFRONT || KS<CF>::CASCADE_LIMIT >= 0) ? e->cont + o : nullptr;
-    a.cont2 = KS<CF>::WAVEFRONT ? e->cont2 + o : nullptr;
-    a.settled = KS<CF>::WAVEFRONT ? e->settled + o : nullptr;
-    a.dead_list = KS<CF>::WAVEFRONT ? e->dead_list + o : nullptr;
+    a.cont = KS<CF>::CASCADE_LIMIT >= 0 ? e->cont + o : nullptr;
     a.cont_stride = e->n;
     if (!sh.czero[par]) HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), st));
     sh.czero[par] = false;
@@ -1866,33 +1516,11 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         const int64_t g = ((int64_t)(sh.n * f) + KS<CF>::B - 1) / KS<CF>::B;
         return dim3((unsigned)(g > 0 ? g : 1));
     };
-    if constexpr (KS<CF>::WAVEFRONT) {
-        // records: begin -> cont, each one-iteration pass -> the other buffer, the tail finishes them;
-        // share of boards still matching after k iterations: 1: ~50 %, 2: ~19 %, 3: ~8 %
-        static constexpr double share[5] = {1.0, 0.6, 0.3, 0.15, 0.08};
-        hipLaunchKernelGGL(k_wf_begin<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
+    hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    if (a.cont) {  // sized for the share of paused steps (~20 % at limit 2)
+        hipLaunchKernelGGL(k_env_cont<CF>, frac_grid(0.25), dim3(KS<CF>::B), 0, st, a);
         HIP_TRY(hipGetLastError());
-        uint32_t* rb[2] = {a.cont, a.cont2};
-        int k = WF<CF>::BEGIN_LIMIT, p = 0;
-        for (; p < WF<CF>::PASSES; ++p, ++k) {
-            hipLaunchKernelGGL(k_wf_pass<CF>, frac_grid(share[k < 4 ? k : 4]), dim3(KS<CF>::B), 0, st, a, rb[p & 1],
-                               &cnt[4 + p], rb[(p + 1) & 1], &cnt[5 + p], 1);
-            HIP_TRY(hipGetLastError());
-        }
-        hipLaunchKernelGGL(k_wf_pass<CF>, frac_grid(share[k < 4 ? k : 4]), dim3(KS<CF>::B), 0, st, a, rb[p & 1],
-                           &cnt[4 + p], (uint32_t*)nullptr, (uint32_t*)nullptr, -1);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_wf_finish<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_wf_dead<CF>, dim3(1), dim3(KS<CF>::B), 0, st, a);
-        HIP_TRY(hipGetLastError());
-    } else {
-        hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
-        HIP_TRY(hipGetLastError());
-        if (a.cont) {  // sized for the share of paused steps (~20 % at limit 2)
-            hipLaunchKernelGGL(k_env_cont<CF>, frac_grid(0.25), dim3(KS<CF>::B), 0, st, a);
-            HIP_TRY(hipGetLastError());
-        }
     }
     hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
     HIP_TRY(hipGetLastError());
@@ -1913,8 +1541,6 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.list_seed = e->pf_seed[par] + o;
         r.list_slot = e->pf_slot[par] + o;
         r.list_count = &cnt[1];
-        r.ovf_count = &cnt[2];
-        r.ovf_list = e->pf_ovf[par] + o;
         r.stats = base + 41;
         prefetch_args<CF>(e, o, r);
         // the grid is sized for the expected number of finished boards and grid-strides
@@ -1985,10 +1611,7 @@ int fill_next_slots(m3_env* e) {
         r.seed_add = k * e->stride;
         r.slot0 = k;
         r.slot_of = e->slot;
-        r.ovf_count = &e->counters[48 + k];
-        r.ovf_list = e->pf_ovf[0];
         prefetch_args<CF>(e, 0, r);
-        HIP_TRY(hipMemsetAsync(r.ovf_count, 0, 4, c->stream));
         int rc = launch_init<CF>(c->stream, r, e->n);
         if (rc) return rc;
     }
@@ -1996,6 +1619,32 @@ int fill_next_slots(m3_env* e) {
     return M3_OK;
 }
 
+// After m3_env_set: rebuild what the env derives from the loaded fields --
+// every board back in episode slot 0, the chain word mt[397] of its seed, the
+// legal set of its board, the queued next episodes -- and restart the step
+// counter, exactly the state m3_env_reset leaves behind for those fields.
+template <class CF>
+int rederive(m3_env* e) {
+    m3_ctx* c = e->ctx;
+    HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));
+    HIP_TRY(hipMemsetAsync(e->slot, 0, e->n, c->stream));
+    const int64_t g = std::min<int64_t>((e->n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_mt397, dim3((unsigned)g), dim3(256), 0, c->stream, e->n, e->seeds, e->m397);
+    HIP_TRY(hipGetLastError());
+    int rc = launch_legal<CF>(c, e->n, e->boards[e->cur], e->legal);
+    if (rc) return rc;
+    e->steps = 0;
+    e->gpend[0] = e->gpend[1] = false;
+    for (auto& sh : e->shards)
+        for (bool& z : sh.czero) z = true;  // (the memset above; this ends with a sync)
+    if (e->autoreset) {
+        rc = fill_next_slots<CF>(e);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    e->stale = false;
+    return M3_OK;
+}
 
 }  // namespace
 
@@ -2011,6 +1660,11 @@ static int with_shape(int shape, F&& f) {
     M3_SHAPES(X)
 #undef X
     return set_err(M3_ERR_UNSUPPORTED, "board shape not compiled in");
+}
+
+static int ensure_fresh(m3_env* e) {
+    if (!e->stale) return M3_OK;
+    return with_shape(e->ctx->shape, [&](auto cf) { return rederive<decltype(cf)>(e); });
 }
 
 extern "C" {
@@ -2111,8 +1765,6 @@ int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boar
     a.boards = d_boards;
     a.draws = d_draws;
     a.first_action = d_first;
-    a.ovf_count = &c->counters[1];
-    a.ovf_list = cv.take<uint32_t>(n);
     rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, n); });
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(out_boards, d_boards, n * c->N, hipMemcpyDeviceToHost, c->stream));
@@ -2344,25 +1996,14 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         alloc(&e->pf_list[p], n * 4);
         alloc(&e->pf_seed[p], n * 4);
         alloc(&e->pf_slot[p], n * 4);
-        alloc(&e->pf_ovf[p], n * 4);
     }
     with_shape(c->shape, [&](auto cf) {
         using K = KS<decltype(cf)>;
         using St = LdsStore<decltype(cf), K::GCAP, K::B>;
         alloc(&e->spill, (size_t)MAX_SHARDS * K::SPILL_RECORDS * St::SPILL_WORDS * 4);
-        if constexpr (!K::CHAIN) {
-            alloc(&e->sraw, (size_t)NSLOT * n * (size_t)K::RAWN * sizeof(typename K::RawT));
-            alloc(&e->sts, (size_t)NSLOT * n * 4ull * K::TS_WORDS);
-            alloc(&e->sacc, (size_t)NSLOT * n * 4ull * K::ACCW);
-        }
         alloc(&e->m397, (size_t)NSLOT * n * 4ull);
         constexpr size_t RW = 1 + EnvCont<decltype(cf)>::WORDS;
-        if constexpr (K::WAVEFRONT || K::CASCADE_LIMIT >= 0) alloc(&e->cont, RW * n * 4ull);
-        if constexpr (K::WAVEFRONT) {
-            alloc(&e->cont2, RW * n * 4ull);
-            alloc(&e->settled, (RW - 1) * n * 4ull);
-            alloc(&e->dead_list, n * 4ull);
-        }
+        if constexpr (K::CASCADE_LIMIT >= 0) alloc(&e->cont, RW * n * 4ull);
         return 0;
     });
     for (hipEvent_t& ev : e->gev)
@@ -2411,7 +2052,9 @@ int m3_env_set_shards(m3_env* e, int nshards) {
 int m3_env_synchronize(m3_env* e) {
     CHECK_ARG(e, "null env");
     HIP_TRY(hipSetDevice(e->ctx->device));
-    return sync_env(e);
+    int rc = sync_env(e);
+    if (rc) return rc;
+    return ensure_fresh(e);
 }
 
 int m3_env_destroy(m3_env* e) {
@@ -2429,12 +2072,12 @@ int m3_env_destroy(m3_env* e) {
     void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->flags, e->draws, e->legal, e->score, e->moves,
                     e->next_action, e->reward, e->done, e->trunc, e->actions[0], e->actions[1], e->counters,
                     e->ovf_list,
-                    e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal, e->sraw, e->sts,
-                    e->sacc, e->spill, e->m397, e->cont, e->cont2, e->settled, e->dead_list};
+                    e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal,
+                    e->spill, e->m397, e->cont};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < PF_LAG; ++q)
-        for (void* p : {(void*)e->pf_list[q], (void*)e->pf_seed[q], (void*)e->pf_slot[q], (void*)e->pf_ovf[q]})
+        for (void* p : {(void*)e->pf_list[q], (void*)e->pf_seed[q], (void*)e->pf_slot[q]})
             if (p) (void)hipFree(p);
     if (e->comm) ncclCommDestroy(e->comm);
     for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
@@ -2472,11 +2115,6 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     a.trunc = e->trunc;
     a.flags = e->flags;
     a.draws = e->draws;
-    a.ovf_count = &e->counters[48];
-    a.ovf_list = e->pf_ovf[0];
-    a.sraw = e->sraw;  // episode slot 0 (null with KS::CHAIN: no stream cache)
-    a.sts = e->sts;
-    a.sacc = e->sacc;
     a.m397 = e->m397;
     a.cstride = e->n;
     HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));  // also clears the stats
@@ -2512,7 +2150,13 @@ int m3_env_step_device(m3_env* e, const int32_t* d_actions) {
     CHECK_ARG(e, "null env");
     if (!e->ready) return set_err(M3_ERR_STATE, "m3_env_step before m3_env_reset");
     HIP_TRY(hipSetDevice(e->ctx->device));
-    return with_shape(e->ctx->shape, [&](auto cf) { return launch_env_step<decltype(cf)>(e, d_actions); });
+    return with_shape(e->ctx->shape, [&](auto cf) {
+        if (e->stale) {
+            const int rc = rederive<decltype(cf)>(e);
+            if (rc) return rc;
+        }
+        return launch_env_step<decltype(cf)>(e, d_actions);
+    });
 }
 
 // Host actions: copied into pinned staging[p] (p = step parity) on the host,
@@ -2581,10 +2225,51 @@ int m3_env_get(m3_env* e, int what, void* host_out) {
     int rc = env_field(e, what, &p, &bytes);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(e->ctx->device));
+    rc = ensure_fresh(e);
+    if (rc) return rc;
     rc = join_shards(e, e->ctx->stream);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(host_out, p, bytes, hipMemcpyDeviceToHost, e->ctx->stream));
     HIP_TRY(hipStreamSynchronize(e->ctx->stream));
+    return M3_OK;
+}
+
+int m3_env_set(m3_env* e, int what, const void* host_in) {
+    CHECK_ARG(e && host_in, "bad arguments");
+    switch (what) {
+        case M3_ENV_BOARDS: case M3_ENV_SEEDS: case M3_ENV_SCORE: case M3_ENV_MOVES: case M3_ENV_NEXT_ACTION:
+        case M3_ENV_REWARD: case M3_ENV_DONE: case M3_ENV_TRUNCATED: case M3_ENV_FLAGS: case M3_ENV_DRAWS:
+            break;
+        default:
+            return set_err(M3_ERR_INVALID, "env field %d is derived, not settable", what);
+    }
+    void* p;
+    size_t bytes;
+    int rc = env_field(e, what, &p, &bytes);
+    if (rc) return rc;
+    if (what == M3_ENV_BOARDS) {
+        const int8_t* b = static_cast<const int8_t*>(host_in);
+        for (size_t i = 0; i < bytes; ++i)
+            if (b[i] < 0) return set_err(M3_ERR_INVALID, "cell value outside [0, 127] at byte %zu", i);
+    }
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    rc = sync_env(e);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(p, host_in, bytes, hipMemcpyHostToDevice));
+    e->stale = true;
+    e->ready = true;
+    return M3_OK;
+}
+
+int m3_env_comm_size(m3_env* e, int* out) {
+    CHECK_ARG(e && out, "bad arguments");
+    if (!e->comm) {
+        *out = 1;
+        return M3_OK;
+    }
+    int n = 0;
+    RCCL_TRY(ncclCommCount(e->comm, &n));
+    *out = n;
     return M3_OK;
 }
 

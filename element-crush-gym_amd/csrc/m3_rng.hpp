@@ -209,187 +209,6 @@ struct MT19937 {
 };
 using FullMT = MT19937<KeyArray>;
 
-// --------------------------------------------------------------------------
-// Per-board stream cache (batched env). Because the reference reseeds with the
-// board's fixed seed at every step, every step of an episode reads the SAME
-// stream, so reset stores it once (k_init):
-//   raw[k]   low bits of raw output k, k < RAWN (RawT is wide enough for every
-//            mask a step applies: 2^BITS-1 for tiles, the shuffle's <= 15 and
-//            the random action's < 2^ceil(log2 A));
-//   ts[p][w] tile stream as bit-planes: tile j = (j-th accepted masked draw)+1
-//            = randint(1, T+1) value j, bit p of tile j at bit j of plane p;
-//   acc[w]   acceptance bitmap of the raw draws (bit k: raw k became a tile).
-// A step then never runs MT19937: the refill deposits whole columns of tiles
-// (m3_rules.hpp, refill_tiles), and the few raw draws of a shuffle or of the
-// next random action are byte loads. Position bookkeeping: in tile mode the
-// raw position after tile j-1 is max(kb, position of the (j-1)-th accepted
-// draw + 1); in raw mode it is k. Anything beyond the cache raises `overflow`
-// and the step is recomputed exactly (FullMT).
-template <class RawT, int RAWN, int BITS, int TSW, int ACCW>
-struct CachedRNG {
-    static constexpr bool TILES = true;
-    static constexpr int TCAP = TSW * 32;
-    static constexpr uint32_t WE = 16u / sizeof(RawT);  // raw entries per 16-byte window
-    const RawT* raw;       // this board's RAWN-entry row (16-byte aligned)
-    const uint32_t* ts;    // plane p, word w at ts[(p * (TSW + 1) + w) * stride] (word TSW is a zero pad)
-    const uint32_t* acc;   // word w at acc[w * stride]
-    int stride;
-    uint32_t cap;          // tiles available: min(TCAP, accepted draws below RAWN)
-    uint32_t kb, j, k, in_tiles, overflow;
-    uint32_t win[4], wlo;  // raw entries [wlo, wlo + WE), one 16-byte load
-
-    M3_HD void load_window(uint32_t at) {
-        wlo = at & ~(WE - 1u);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(raw + wlo);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) win[i] = src[i];
-    }
-    M3_HD void init(const RawT* r, const uint32_t* t, const uint32_t* a, int st) {
-        raw = r;
-        ts = t;
-        acc = a;
-        stride = st;
-        load_window(0u);  // issued early: the random action usually reads the first few entries
-        uint32_t n = 0;
-#pragma unroll
-        for (int w = 0; w < ACCW; ++w) n += (uint32_t)__builtin_popcount(acc[w * stride]);
-        cap = n < (uint32_t)TCAP ? n : (uint32_t)TCAP;
-        overflow = 0u;
-        reseed();
-    }
-    M3_HD void reseed() {
-        kb = 0u;
-        j = 0u;
-        k = 0u;
-        in_tiles = 1u;
-    }
-    // raw position of the draw after the (jj-1)-th accepted one (jj >= 1)
-    M3_HD uint32_t after_tile(uint32_t jj) const {
-        uint32_t r = jj - 1u, word = 0u, wi = (uint32_t)ACCW;
-        bool found = false;
-#pragma unroll
-        for (int w = 0; w < ACCW; ++w) {
-            const uint32_t a = acc[w * stride];
-            const uint32_t c = (uint32_t)__builtin_popcount(a);
-            const bool here = !found && r < c;
-            word = here ? a : word;
-            wi = here ? (uint32_t)w : wi;
-            r = (found || here) ? r : r - c;
-            found = found || here;
-        }
-        if (!found) return (uint32_t)RAWN + 1u;
-        return 32u * wi + (uint32_t)select_bit(word, (int)r) + 1u;
-    }
-    M3_HD uint32_t draws() const {
-        if (!in_tiles) return k;
-        if (j == 0u) return kb;
-        const uint32_t p = after_tile(j);
-        return p > kb ? p : kb;
-    }
-    M3_HD uint32_t next32() {
-        if (in_tiles) {
-            k = draws();
-            in_tiles = 0u;
-        }
-        if (k >= (uint32_t)RAWN) {
-            overflow = 1u;
-            return 0u;
-        }
-        if (k - wlo >= WE) load_window(k);
-        const uint32_t e = k - wlo;
-        k += 1u;
-        constexpr uint32_t PER = 4u / sizeof(RawT), SH = 8u * sizeof(RawT);
-        const uint32_t q = e / PER;
-        uint32_t wv = 0u;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) wv |= win[i] & (0u - (uint32_t)(q == (uint32_t)i));
-        return (wv >> (SH * (e % PER))) & ((1u << SH) - 1u);
-    }
-    // switch to tile mode at the current raw position
-    M3_HD void begin_tiles() {
-        if (in_tiles) return;
-        kb = k;
-        uint32_t n = 0;
-#pragma unroll
-        for (int w = 0; w < ACCW; ++w) {
-            const int lo = 32 * w;
-            const uint32_t a = acc[w * stride];
-            uint32_t m = 0xFFFFFFFFu;
-            if ((int)k < lo) m = 0u;
-            else if ((int)k < lo + 32) m = (1u << (k - (uint32_t)lo)) - 1u;
-            n += (uint32_t)__builtin_popcount(a & m);
-        }
-        j = n;
-        in_tiles = 1u;
-    }
-    // 32 bits of tile plane p starting at tile jj (jj < TCAP)
-    M3_HD uint32_t tile_bits(int p, uint32_t jj) const {
-        const uint32_t q = jj >> 5, s = jj & 31u;
-        const uint32_t lo = ts[(p * (TSW + 1) + (int)q) * stride];
-        const uint32_t hi = ts[(p * (TSW + 1) + (int)q + 1) * stride];
-        return s ? ((lo >> s) | (hi << (32u - s))) : lo;
-    }
-};
-
-template <class G, class = void>
-struct HasTiles {
-    static constexpr bool value = false;
-};
-template <class G>
-struct HasTiles<G, std::void_t<decltype(G::TILES)>> {
-    static constexpr bool value = true;
-};
-
-// Fill a stream cache from seed s (RAWN raw outputs of seed(s)); used by reset.
-// raw_out(k, v) receives every raw output; ts/acc words are returned through
-// the callbacks so the caller chooses the memory layout.
-template <int RAWN, int BITS, int TSW, int ACCW, uint32_t TILE_MASK, uint32_t TILE_RNG, class RawF, class TsF,
-          class AccF>
-M3_HD void build_stream_cache(uint32_t seed, uint32_t m397, RawF raw_out, TsF ts_out, AccF acc_out) {
-    static_assert(TILE_RNG > 0u, "randint(1, 2) consumes no draws: no tile stream");
-    static_assert(RAWN == 32 * ACCW && RAWN <= 624, "cache geometry");
-    ChainMTT<624u> g;
-    g.init(seed, m397);
-    uint32_t tp[BITS];
-#pragma unroll
-    for (int p = 0; p < BITS; ++p) tp[p] = 0u;
-    uint32_t accw = 0u, nt = 0u;
-    for (int k = 0; k < RAWN; ++k) {
-        const uint32_t v = g.next32();
-        raw_out(k, v);
-        const uint32_t t = v & TILE_MASK;
-        if (t <= TILE_RNG) {
-            accw |= 1u << (k & 31);
-            if (nt < (uint32_t)(TSW * 32)) {
-                const uint32_t val = t + 1u;
-#pragma unroll
-                for (int p = 0; p < BITS; ++p) tp[p] |= ((val >> p) & 1u) << (nt & 31u);
-                ++nt;
-                if ((nt & 31u) == 0u) {
-#pragma unroll
-                    for (int p = 0; p < BITS; ++p) {
-                        ts_out(p, (int)(nt >> 5) - 1, tp[p]);
-                        tp[p] = 0u;
-                    }
-                }
-            }
-        }
-        if ((k & 31) == 31) {
-            acc_out(k >> 5, accw);
-            accw = 0u;
-        }
-    }
-    if (nt < (uint32_t)(TSW * 32)) {
-#pragma unroll
-        for (int p = 0; p < BITS; ++p) ts_out(p, (int)(nt >> 5), tp[p]);
-        for (int w = (int)(nt >> 5) + 1; w < TSW; ++w)
-#pragma unroll
-            for (int p = 0; p < BITS; ++p) ts_out(p, w, 0u);
-    }
-#pragma unroll
-    for (int p = 0; p < BITS; ++p) ts_out(p, TSW, 0u);  // pad
-}
-
 // RandomState.randint(low, low+rng+1) for one element (legacy masked rejection):
 // returns v in [0, rng]. rng == 0 consumes no draw (numpy's rng == 0 fast path).
 template <class G>

@@ -83,23 +83,10 @@ struct Cfg {
     using G = Geo<R, C, W>;
 };
 
-// Geometry of the batched env's per-board stream cache (m3_rng.hpp,
-// CachedRNG): RAWN raw outputs (RawT holds every mask a step applies: tiles
-// 2^BITS-1, shuffle <= 15, random action < 2^ceil(log2 A)), TSW words of tile
-// stream per plane, ACCW words of acceptance bitmap.
 // boards of at least this many words take the word-sliced legal_masks (0: never)
 #ifndef M3_LEGAL_SLICED_W
 #define M3_LEGAL_SLICED_W 5
 #endif
-
-template <class CF>
-struct StreamCache {
-    static constexpr int RAWN = CF::N > 128 ? 512 : 320;
-    static constexpr int ACCW = RAWN / 32;
-    static constexpr int TSW = CF::N > 128 ? 8 : 5;
-    using RawT = std::conditional_t<(CF::A > 256), uint16_t, uint8_t>;
-    using Rng = CachedRNG<RawT, RAWN, CF::BITS, TSW, ACCW>;
-};
 
 // --------------------------------------------------------------------------
 // small helpers
@@ -652,47 +639,11 @@ M3_HD typename CF::Bd gravity(typename CF::Bd* P) {
     return VALID.andnot(occ);
 }
 
-// Refill from a cached tile stream (CachedRNG): column c takes the next h_c
-// tiles, tile s_c + r going to row r (new[0] on top), so a column is one
-// funnel-shift extract per plane and a fixed deposit of its R bits -- no
-// MT19937, no rejection loop, no per-tile divergence.
-template <class CF, class RNG>
-M3_HD void refill_tiles(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng) {
-    using G = typename CF::G;
-    constexpr int C = CF::C, R = CF::R;
-    rng.begin_tiles();
-    uint32_t j = rng.j;
-    if (j + (uint32_t)em.popc() > rng.cap) {
-        rng.overflow = 1u;
-        return;
-    }
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        const int h = (em & G::col_eq(c)).popc();
-        const uint32_t hm = (h >= 32) ? 0xFFFFFFFFu : ((1u << h) - 1u);
-#pragma unroll
-        for (int p = 0; p < CF::BITS; ++p) {
-            const uint32_t f = rng.tile_bits(p, j) & hm;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int x = r * C + c;
-                P[p].w[x >> 5] |= ((f >> r) & 1u) << (x & 31);
-            }
-        }
-        j += (uint32_t)h;
-    }
-    rng.j = j;
-}
-
 // refill of the top-aligned empty cells em
 template <class CF, class RNG>
 M3_HD void refill(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng) {
     using Bd = typename CF::Bd;
     constexpr int C = CF::C, R = CF::R;
-    if constexpr (HasTiles<RNG>::value) {
-        refill_tiles<CF>(P, em, rng);
-        return;
-    }
     if (!em.any()) return;
     uint32_t tops = em.w[0] & ((1u << C) - 1u);  // columns with at least one empty cell
     int c = __builtin_ctz(tops);
@@ -1060,8 +1011,8 @@ M3_HD void init_board(typename CF::Bd* P, RNG& mt) {
 // funnel shift of the stream's plane words) plus one masked merge. The
 // stream is generated as it is needed (one raw draw per loop trip, tiles
 // appended to plane words in `tm`, plane p word w at tm[(p*TWMAX + w)*stride]).
-// Raw outputs k < rawn and their acceptance bits go to the sinks, which is
-// exactly the step's stream cache (StreamCache), so a reset builds it for free.
+// Raw outputs k < rawn and their acceptance bits go to the sinks (the
+// kernels pass rawn = 0; the host harness uses them to check the stream).
 // Returns false if the board needs more than the first MT block (624 draws):
 // the caller recomputes it. `draws` = raw outputs consumed by __init__.
 // --------------------------------------------------------------------------

@@ -35,8 +35,8 @@ EXPORTS = [
     "m3_init_boards", "m3_apply_actions", "m3_legal_actions", "m3_rollouts", "m3_rollouts_device",
     "m3_env_create", "m3_env_destroy", "m3_env_reset", "m3_env_set_shards", "m3_env_synchronize",
     "m3_env_set_autoreset", "m3_env_step",
-    "m3_env_step_device", "m3_env_get", "m3_env_device_ptr",
-    "m3_comm_unique_id", "m3_env_comm_init", "m3_env_gather", "m3_env_gather_device", "m3_env_debug_stall",
+    "m3_env_step_device", "m3_env_get", "m3_env_set", "m3_env_device_ptr",
+    "m3_comm_unique_id", "m3_env_comm_init", "m3_env_comm_size", "m3_env_gather", "m3_env_gather_device", "m3_env_debug_stall",
     "m3_env_stats", "m3_env_timing",
     "m3_env_kernel_ms",
 ]
@@ -88,7 +88,9 @@ def lib():
             "m3_env_step": ([vp, vp], i32),
             "m3_env_step_device": ([vp, vp], i32),
             "m3_env_get": ([vp, i32, vp], i32),
+            "m3_env_set": ([vp, i32, vp], i32),
             "m3_env_device_ptr": ([vp, i32, vp], i32),
+            "m3_env_comm_size": ([vp, vp], i32),
             "m3_comm_unique_id": ([vp], i32),
             "m3_env_comm_init": ([vp, vp, i32, i32], i32),
             "m3_env_gather": ([vp, vp], i32),

@@ -19,6 +19,12 @@ re-initialised in the same step with seed += seed_stride; ``done`` and
 Multi-GPU: one process per GPU, each owning its own boards (no data exchange
 during a step). ``init_comm()`` + ``gather()`` do one RCCL all-gather of the
 packed (reward << 2 | truncated << 1 | done) words over xGMI.
+
+Checkpoint / resume: ``save(path)`` writes every board's state (the
+reference's BoardV2 state (array, cfg.seed, n_actions, _reward) plus
+Match3Env's score / moves_taken and the pre-drawn next action) to one .npz;
+``BatchedMatch3Env.load(path)`` builds an env that steps on exactly as the
+saved one would have (m3_env_set, include/m3.h).
 """
 from __future__ import annotations
 
@@ -46,7 +52,9 @@ class BatchedMatch3Env:
         self.set_autoreset(autoreset, stride)
         if shards is not None:
             self.set_shards(shards)
-        self.reset(seeds=seeds, seed_base=seed_base)
+        self.nranks = 1
+        if seeds is not False:  # (load() fills the state instead)
+            self.reset(seeds=seeds, seed_base=seed_base)
 
     # ---- lifecycle -------------------------------------------------------------------
     def close(self):
@@ -64,6 +72,7 @@ class BatchedMatch3Env:
 
     def set_autoreset(self, enabled: bool, seed_stride: int):
         check(lib().m3_env_set_autoreset(self.handle, int(bool(enabled)), int(seed_stride) & 0xFFFFFFFF))
+        self.autoreset, self.seed_stride = bool(enabled), int(seed_stride) & 0xFFFFFFFF
 
     def reset(self, seeds=None, seed_base: int = 1):
         """Match3Env.reset for every board; seeds default to seed_base + i."""
@@ -154,6 +163,44 @@ class BatchedMatch3Env:
     def draws(self):
         return self._get(_native.ENV_DRAWS, np.uint32, (self.n,))
 
+    # ---- checkpoint / resume ------------------------------------------------------------
+    _STATE = (("boards", _native.ENV_BOARDS, np.int8), ("seeds", _native.ENV_SEEDS, np.uint32),
+              ("score", _native.ENV_SCORE, np.int32), ("moves", _native.ENV_MOVES, np.int32),
+              ("next_action", _native.ENV_NEXT_ACTION, np.int32), ("reward", _native.ENV_REWARD, np.int32),
+              ("done", _native.ENV_DONE, np.uint8), ("truncated", _native.ENV_TRUNCATED, np.uint8),
+              ("flags", _native.ENV_FLAGS, np.uint32), ("draws", _native.ENV_DRAWS, np.uint32))
+
+    def state_dict(self) -> dict:
+        """Every board's resumable state (host copies) + the env's configuration."""
+        shapes = {"boards": (self.n, self.rows, self.columns)}
+        st = {k: self._get(w, dt, shapes.get(k, (self.n,))) for k, w, dt in self._STATE}
+        st["config"] = np.array([self.n, self.rows, self.columns, self.types, self.num_moves, self.env_goal,
+                                 int(self.autoreset), self.seed_stride], dtype=np.int64)
+        return st
+
+    def load_state_dict(self, st: dict):
+        cfg = [int(x) for x in st["config"]]
+        if cfg[:6] != [self.n, self.rows, self.columns, self.types, self.num_moves, self.env_goal]:
+            raise ValueError(f"checkpoint is for env {cfg[:6]}, not "
+                             f"{[self.n, self.rows, self.columns, self.types, self.num_moves, self.env_goal]}")
+        self.set_autoreset(bool(cfg[6]), cfg[7])
+        for k, w, dt in self._STATE:
+            a = np.ascontiguousarray(st[k], dtype=dt)
+            check(lib().m3_env_set(self.handle, w, ptr(a)))
+        return self
+
+    def save(self, path):
+        np.savez(path, **self.state_dict())
+
+    @classmethod
+    def load(cls, path, device: int = 0, shards: int = None) -> "BatchedMatch3Env":
+        with np.load(path, allow_pickle=False) as f:
+            st = {k: f[k] for k in f.files}
+        n, rows, columns, types, num_moves, env_goal, autoreset, stride = (int(x) for x in st["config"])
+        env = cls(n, rows, columns, types, num_moves=num_moves, env_goal=env_goal, device=device, seeds=False,
+                  autoreset=bool(autoreset), seed_stride=stride, shards=shards)
+        return env.load_state_dict(st)
+
     def device_ptr(self, what) -> int:
         p = ctypes.c_void_p()
         check(lib().m3_env_device_ptr(self.handle, what, ctypes.byref(p)))
@@ -170,6 +217,12 @@ class BatchedMatch3Env:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
         check(lib().m3_env_comm_init(self.handle, buf, int(nranks), int(rank)))
         self.nranks = nranks
+
+    def comm_size(self) -> int:
+        """Ranks of the env's RCCL communicator as RCCL reports them (1 before init_comm)."""
+        n = ctypes.c_int(0)
+        check(lib().m3_env_comm_size(self.handle, ctypes.byref(n)))
+        return n.value
 
     def gather(self, to_host: bool = False):
         """RCCL all-gather of packed reward/truncated/done of every board of every rank."""

@@ -46,6 +46,7 @@ class BoardV2(State):
         self.n_actions = n_actions
         self._reward = 0
         if array is None:
+            np.random.seed(cfg.seed)  # boardv2.py:20 -- raises ValueError outside [0, 2**32) like the reference
             boards, draws, _ = _ctx(cfg).init_boards([int(cfg.seed) & 0xFFFFFFFF])
             self.array = boards[0].astype(np.int64)
             _sync_global_rng(cfg.seed, int(draws[0]))       # boardv2.py:20-27 leave the RNG here

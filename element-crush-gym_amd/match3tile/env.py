@@ -78,7 +78,9 @@ class Match3Env:
         self.score, self.moves_taken = 0, 0
         self.actions = []
         self.board = self._new_board()
-        n_act = self.board.cfg.action_space
+        # env.py:36 counts adjacent cell pairs; it equals BoardConfig.action_space (the id
+        # range apply_action accepts) on square boards only -- kept as the reference has it
+        n_act = height * (width - 1) + width * (height - 1)
         if _spaces is not None:
             self.action_space = _spaces.Discrete(n_act)
             self.observation_space = _spaces.Box(0, self.board.cfg.mega_token, (height, width), np.int64)

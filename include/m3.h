@@ -158,11 +158,26 @@ int m3_env_step_device(m3_env *env, const int32_t *d_actions);
 int m3_env_get(m3_env *env, int what, void *host_out);
 int m3_env_device_ptr(m3_env *env, int what, void **out);
 
+/* Checkpoint / resume of the batched env (the reference state is
+ * (array, cfg.seed, n_actions, _reward), boardv2.py:12-16, plus Match3Env's
+ * score and moves_taken, env.py:34). Overwrites one field of every board from
+ * host memory laid out as m3_env_get returns it. Settable: M3_ENV_BOARDS,
+ * SEEDS, SCORE, MOVES, NEXT_ACTION and the last step's REWARD, DONE,
+ * TRUNCATED, FLAGS, DRAWS; LEGAL and GATHERED are derived (M3_ERR_INVALID).
+ * The per-board state the env derives from these -- the legal set of the
+ * board, the MT19937 chain word mt[397] of the seed, the queued autoreset
+ * episodes -- is rebuilt before the next step / get / synchronize, so an env
+ * loaded with another env's fields steps exactly as that env would have. A
+ * freshly created env may be loaded instead of reset. */
+int m3_env_set(m3_env *env, int what, const void *host_in);
+
 /* ---- multi-GPU: RCCL over xGMI, one process per GPU --------------------- */
 /* 128-byte ncclUniqueId; rank 0 creates it, the caller ships it to all ranks. */
 int m3_comm_unique_id(uint8_t out_id[128]);
 /* One communicator per env; a second call returns M3_ERR_STATE. */
 int m3_env_comm_init(m3_env *env, const uint8_t id[128], int nranks, int rank);
+/* Ranks of the env's communicator as RCCL reports them (ncclCommCount); 1 before m3_env_comm_init. */
+int m3_env_comm_size(m3_env *env, int *out_nranks);
 /* ncclAllGather of the last step's packed (reward << 2 | truncated << 1 | done)
  * int32 words of every board of every rank into the env's device buffer
  * M3_ENV_GATHERED ([nranks][n], rank-major); host_out (nullable, int32[nranks*n])

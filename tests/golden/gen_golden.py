@@ -18,6 +18,9 @@ Files written:
                   incl. specials, all combo pairs, typed specials, illegal swaps, terminal boards
   episodes.npz    samplerTasks.random_task-style seeded episodes (actions, rewards, draws, final board)
   shuffle.npz     dead-board transitions that terminate (shuffle path) + seeds that cycle forever
+  env.npz         Match3Env runs of the README.md:18-31 loop (env.board.random_action(), step,
+                  reset at done with and without a seed), bookkeeping restated over the reference
+                  BoardV2 (env.py cannot run at the snapshot): obs/reward/done/truncated per step
 """
 from __future__ import annotations
 
@@ -228,6 +231,98 @@ def gen_episodes(pool):
     np.savez_compressed(os.path.join(OUT, "episodes.npz"), **out)
 
 
+# --------------------------------------------------------------------------- env
+class _RefEnv:
+    """Match3Env (env.py:8-65) restated over the REAL reference BoardV2.
+
+    The reference class itself cannot run (env.py:38,64 pass a `seed` keyword
+    BoardV2 does not take; env.py:50 unpacks a BoardV2), so only its
+    bookkeeping is restated here: everything a step computes -- the board, its
+    reward, the global RNG the next random action draws from -- comes from the
+    reference's own BoardV2 / BoardConfig / numpy."""
+
+    def __init__(self, width, height, num_types, num_moves, env_goal, seed):
+        self.width, self.height, self.num_types = width, height, num_types
+        self.num_moves, self.env_goal = num_moves, env_goal
+        self.seed = seed
+        self.score, self.moves_taken = 0, 0
+        self.action_space = height * (width - 1) + width * (height - 1)          # env.py:36
+        self.board = self._board()
+
+    def _board(self):
+        return BoardV2(self.num_moves, BoardConfig(seed=self.seed, rows=self.height, columns=self.width,
+                                                   types=self.num_types))
+
+    def step(self, action):                                                       # env.py:48-56
+        before = self.board.reward
+        self.board = self.board.apply_action(action)
+        reward = int(self.board.reward - before)
+        self.score += reward
+        self.moves_taken += 1
+        truncated = self.score >= self.env_goal
+        done = truncated or self.num_moves == self.moves_taken
+        return self.board.array, reward, done, truncated, {}
+
+    def reset(self, seed=None):                                                   # env.py:58-65
+        self.seed = seed if seed is not None else (1 + self.seed) % 2 ** 32 - 1
+        self.score, self.moves_taken = 0, 0
+        self.board = self._board()
+        return self.board.array, {}
+
+
+def _env_run(args):
+    """The README.md:18-31 loop: action = env.board.random_action() (= np.random.choice(
+    board.legal_actions) from numpy's global stream, samplerTasks.py:13), step, reset at done
+    with the next entry of `resets` (-1: reset() without a seed, the env.py:62 quirk)."""
+    R, C, T, seed, moves, goal, n_steps, resets = args
+    env = _RefEnv(C, R, T, moves, goal, int(seed))
+    out = dict(init=env.board.array.astype(np.int8), action=[], obs=[], reward=[], done=[], trunc=[],
+               reset_arg=[], reset_obs=[], seed_after=[])
+    resets = list(resets)
+    for _ in range(n_steps):
+        a = int(np.random.choice(env.board.legal_actions))
+        obs, r, done, tr, _ = env.step(a)
+        out["action"].append(a)
+        out["obs"].append(obs.astype(np.int8))
+        out["reward"].append(r)
+        out["done"].append(done)
+        out["trunc"].append(tr)
+        if done:
+            arg = resets.pop(0) if resets else -1
+            o2, _ = env.reset(None if arg < 0 else int(arg))
+            out["reset_arg"].append(arg)
+            out["reset_obs"].append(o2.astype(np.int8))
+        else:
+            out["reset_arg"].append(-2)
+            out["reset_obs"].append(np.zeros((R, C), np.int8))
+        out["seed_after"].append(env.seed)
+    return out
+
+
+def gen_env(pool, shapes=None):
+    rng = np.random.default_rng(2024)
+    out = {}
+    plan = [(20, 500), (20, 150), (7, 10**9), (12, 300)]
+    for (R, C, T), n_runs, n_steps in shapes or [((9, 9, 6), 48, 60), ((16, 16, 8), 16, 45)]:
+        args = []
+        for i in range(n_runs):
+            moves, goal = plan[i % len(plan)]
+            resets = [int(rng.integers(1, 2**32 - 1)) if rng.random() < 0.5 else -1 for _ in range(8)]
+            args.append((R, C, T, int(rng.integers(1, 2**32 - 1)), moves, goal, n_steps, resets))
+        res = pool.map(_env_run, args, chunksize=2)
+        tag = f"{R}x{C}x{T}"
+        out[f"seed_{tag}"] = np.array([a[3] for a in args], dtype=np.uint32)
+        out[f"moves_{tag}"] = np.array([a[4] for a in args], dtype=np.int32)
+        out[f"goal_{tag}"] = np.array([a[5] for a in args], dtype=np.int64)
+        out[f"init_{tag}"] = np.array([r["init"] for r in res])
+        for k, dt in (("action", np.int32), ("obs", np.int8), ("reward", np.int32), ("done", np.uint8),
+                      ("trunc", np.uint8), ("reset_arg", np.int64), ("reset_obs", np.int8),
+                      ("seed_after", np.int64)):
+            out[f"{k}_{tag}"] = np.array([r[k] for r in res], dtype=dt)
+        out[f"action_space_{tag}"] = np.int64(R * (C - 1) + C * (R - 1))
+    np.savez_compressed(os.path.join(OUT, "env.npz"), **out)
+
+
 # ------------------------------------------------------------------------- steps
 def _step_case(args):
     R, C, T, board, seed, n_actions, action = args
@@ -420,6 +515,8 @@ def main():
                 gen_episodes(pool)
             elif w == "shuffle":
                 gen_shuffle(pool)
+            elif w == "env":
+                gen_env(pool)
 
 
 if __name__ == "__main__":

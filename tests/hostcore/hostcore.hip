@@ -93,71 +93,6 @@ static int step_one(typename CF::Bd* P, const int8_t* board, uint32_t seed, int 
     return r;
 }
 
-// The batched-env path: stream cache built as at reset, CachedRNG for the
-// step, exact FullMT recompute when the cache or the group table overflows.
-template <class CF>
-static int step_cached(typename CF::Bd* P, const int8_t* board, uint32_t seed, int na, int act, uint32_t& f,
-                       int32_t& draws, uint32_t* legal, int32_t& next_act, int& recomputed) {
-    using SC = StreamCache<CF>;
-    alignas(16) typename SC::RawT raw[SC::RAWN];
-    typename SC::RawT raw2[SC::RAWN];
-    uint32_t ts[CF::BITS * (SC::TSW + 1)], acc[SC::ACCW], ts2[CF::BITS * (SC::TSW + 1)], acc2[SC::ACCW];
-    // the cache as reset builds it (init_board_tiles) ...
-    {
-        static uint32_t tm[CF::BITS * TileGen<CF>::TWMAX], pos[TileGen<CF>::MAXR];
-        memset(tm, 0, sizeof(tm));
-        typename CF::Bd Q[CF::NP];
-        ChainMT g;
-        g.init(seed, mt_state397(seed));
-        uint32_t d;
-        init_board_tiles<CF>(Q, g, tm, pos, 1, d, (uint32_t)SC::RAWN,
-                             [&](uint32_t k, uint32_t v) { raw[k] = (typename SC::RawT)v; },
-                             [&](uint32_t w, uint32_t v) { acc[w] = v; });
-        for (int p = 0; p < CF::BITS; ++p) {
-            for (int w = 0; w < SC::TSW; ++w) ts[p * (SC::TSW + 1) + w] = tm[p * TileGen<CF>::TWMAX + w];
-            ts[p * (SC::TSW + 1) + SC::TSW] = 0u;
-        }
-    }
-    // ... must equal the straightforward construction
-    build_stream_cache<SC::RAWN, CF::BITS, SC::TSW, SC::ACCW, CF::TILE_MASK, CF::TILE_RNG>(
-        seed, mt_state397(seed), [&](int k, uint32_t v) { raw2[k] = (typename SC::RawT)v; },
-        [&](int p, int w, uint32_t v) { ts2[p * (SC::TSW + 1) + w] = v; }, [&](int w, uint32_t v) { acc2[w] = v; });
-    const uint32_t tiles = [&] { uint32_t c = 0; for (int w = 0; w < SC::ACCW; ++w) c += __builtin_popcount(acc2[w]); return c; }();
-    if (memcmp(raw, raw2, sizeof(raw)) || memcmp(acc, acc2, sizeof(acc))) recomputed += 1 << 20;  // flag: cache mismatch
-    for (int p = 0; p < CF::BITS; ++p)
-        for (uint32_t t = 0; t < tiles && t < (uint32_t)(32 * SC::TSW); ++t)
-            if (((ts[p * (SC::TSW + 1) + (t >> 5)] ^ ts2[p * (SC::TSW + 1) + (t >> 5)]) >> (t & 31)) & 1u)
-                recomputed += 1 << 20;
-    typename SC::Rng rng;
-    rng.init(raw, ts, acc, 1);
-    SmallStore<CF, 8> ss;
-    typename CF::Bd HL, VL;
-    int r = apply_action<CF>(P, na, act, rng, f, HL, VL, ss);
-    uint32_t act_bits[CF::AW];
-    bool redo = (f & FLAG_RECOMPUTE) != 0;
-    if (!redo) {
-        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)rng.draws();
-        action_bits<CF>(HL, VL, act_bits);
-        next_act = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act_bits, rng);
-        redo = rng.overflow != 0u;
-    }
-    if (redo) {
-        recomputed++;
-        FullMT* fm = new FullMT;
-        ArrayStore<CF>* as = new ArrayStore<CF>;
-        load_planes<CF>(board, P);
-        fm->init(seed, 0);
-        r = apply_action<CF>(P, na, act, *fm, f, HL, VL, *as);
-        draws = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? 0 : (int32_t)fm->k;
-        action_bits<CF>(HL, VL, act_bits);
-        next_act = (f & (FLAG_TERMINAL | FLAG_BAD_ACTION)) ? -1 : random_action<CF>(act_bits, *fm);
-        delete fm;
-        delete as;
-    }
-    if (legal) memcpy(legal, act_bits, sizeof(act_bits));
-    return r;
-}
-
 static long g_paused = 0;  // steps that paused in the bounded-cascade mode (hc_paused)
 
 template <class CF>
@@ -185,9 +120,6 @@ static int apply_n(long n, const int8_t* boards, const uint32_t* seeds, const in
             SmallStore<CF, 4> ss;
             rew[i] = step_one<CF, SmallStore<CF, 4>, ChainMT1>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss,
                                                               f, draws[i], lg, next_act[i], recomputed);
-        } else if (small == 16) {  // batched env path: stream cache + CachedRNG
-            rew[i] = step_cached<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], f, draws[i], lg,
-                                     next_act[i], recomputed);
         } else if (small == 8) {  // the 9x9 device table size
             SmallStore<CF, 8> ss;
             rew[i] = step_one<CF>(P, boards + i * CF::N, seeds[i], nact[i], acts[i], ss, f, draws[i], lg,

@@ -21,8 +21,20 @@ class DeviceBuffer:
     """Test-side device memory through the HIP runtime libm3.so itself runs on (no torch: a second
     HIP runtime in the process is not reliable)."""
 
+    @staticmethod
+    def _hip_runtime():
+        """The libamdhip64 that libm3.so itself loaded (read from /proc/self/maps), so the test
+        allocates through the same runtime whatever its soname."""
+        from match3tile import _native
+
+        _native.lib()
+        with open("/proc/self/maps") as f:
+            paths = {line.split()[-1] for line in f if "libamdhip64.so" in line}
+        assert len(paths) == 1, paths
+        return ctypes.CDLL(paths.pop())
+
     def __init__(self, nbytes):
-        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.hip = self._hip_runtime()
         self.nbytes = nbytes
         self.ptr = ctypes.c_void_p()
         assert self.hip.hipMalloc(ctypes.byref(self.ptr), ctypes.c_size_t(nbytes)) == 0

@@ -121,43 +121,6 @@ def _check_steps(hc, g, tag, small):
     assert (drw[live] == g["draws_" + tag][live]).all()
 
 
-@pytest.mark.parametrize("tag", list(SHAPES))
-def test_stream_cache_path_golden(golden, tag):
-    """The batched env's step (stream cache + column refill + cached raw draws) on every step,
-    shuffle and episode fixture, with the exact recompute when the cache overflows."""
-    hc = HostCore(*SHAPES[tag])
-    _check_steps(hc, golden("steps"), tag, 16)
-    _check_steps(hc, golden("shuffle"), tag, 16)
-    e = golden("episodes")
-    seeds = e["seeds_" + tag].astype(np.uint32)
-    b, _, _, act = hc.init(seeds)
-    for m in range(20):
-        assert (act == e["actions_" + tag][:, m]).all()
-        b, rew, drw, _, _, act = hc.apply(b, seeds, 20 - m, act, small=16)
-        assert (rew == e["rewards_" + tag][:, m]).all()
-        assert (drw == e["draws_" + tag][:, m]).all()
-    assert (b == e["final_" + tag].reshape(len(b), -1)).all()
-
-
-@pytest.mark.parametrize("tag", list(SHAPES))
-def test_stream_cache_path_random_states(tag):
-    """Cached path == exact path (FullMT + unbounded group table) on random boards with specials."""
-    R, C, T = SHAPES[tag]
-    hc = HostCore(R, C, T)
-    rng = np.random.default_rng(5)
-    n = 4000 if R == 9 else 600
-    seeds = rng.integers(1, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
-    boards, _, _, _ = hc.init(seeds)
-    cfg = {"9x9x6": (8, 16, 24, 32, 11, 19, 27, 40, 56, 0), "16x16x8": (16, 32, 48, 64, 19, 35, 51, 0)}[tag]
-    sprinkle = rng.random((n, R * C)) < 0.06
-    boards = np.where(sprinkle, rng.choice(cfg, size=(n, R * C)), boards).astype(np.int8)
-    acts = rng.integers(0, R * (C - 1) * 2, size=n)
-    a = hc.apply(boards, seeds, 20, acts)
-    b = hc.apply(boards, seeds, 20, acts, small=16)
-    for x, y in zip(a, b):
-        assert (x == y).all()
-
-
 def test_one_level_chain_fallback_is_exact(golden):
     """The 16x16 env step runs the one-level MT chain (draws < 227): steps past it -- near-full-board
     refills such as mega+mega (256 cells) -- must be redone exactly (rare-branch test, forced by the
