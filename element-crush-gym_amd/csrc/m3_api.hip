@@ -1,40 +1,12 @@
-// m3_api.hip -- gfx950 kernels + the C ABI of include/m3.h.
-//
-// Kernel shape (all step kernels): one board per lane, one-wave (64-lane)
-// workgroups. Boards are int8 [n][R*C] in HBM. A wave stages its 64 boards
-// HBM -> LDS with 16-byte coalesced loads; each lane reads its own board out
-// of LDS as dwords and transposes it into 7 bit-planes in VGPRs, runs the
-// whole fixed-point step in registers (m3_rules.hpp), writes the result back
-// into its LDS slot, and the wave streams the boards out with 16-byte stores.
-// Per-board scalars (seed, mt[397], score, moves, pre-drawn action) are SoA
-// and coalesced.
-//
-// The step's MT19937 is a register-only chain (m3_rng.hpp, ChainMT). A step
-// that needs more draws than the chain reaches, or more match groups than the
-// LDS table + spill pool hold, appends its index to an overflow list and is
-// redone by k_*_fix with the 624-word FullMT in scratch. That kernel reads the
-// untouched input buffer (boards ping-pong), so the result is still exact.
-#include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
+// m3_api.hip -- the C ABI of include/m3.h (kernels and launchers: m3_kernels.hpp).
+#include "m3_kernels.hpp"
 
-#include <stdarg.h>
-#include <stdio.h>
-#include <string.h>
-
-#include <algorithm>
 #include <string>
-#include <vector>
-
-#include "../../include/m3.h"
-#include "m3_rules.hpp"
-
-using namespace m3;
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int set_err(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -45,1333 +17,28 @@ int set_err(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                            \
-    do {                                                                                         \
-        hipError_t e_ = (expr);                                                                  \
-        if (e_ != hipSuccess)                                                                    \
-            return set_err(M3_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
-                           __LINE__);                                                            \
-    } while (0)
-
-#define RCCL_TRY(expr)                                                                            \
-    do {                                                                                          \
-        ncclResult_t r_ = (expr);                                                                 \
-        if (r_ != ncclSuccess) return set_err(M3_ERR_RCCL, "%s: %s", #expr, ncclGetErrorString(r_)); \
-    } while (0)
-
-#define CHECK_ARG(cond, msg)                                       \
-    do {                                                           \
-        if (!(cond)) return set_err(M3_ERR_INVALID, "%s", (msg)); \
-    } while (0)
-
-constexpr int BLOCK = 256;
-constexpr int FIX_BLOCK = 64;
-constexpr int FIX_GRID = 16;       // step fixup almost never has work: few blocks schedule fast
-constexpr int INIT_FIX_BLOCK = 64;
-constexpr int INIT_BLOCK = 64;
-// 9x9: k_init redoes its few >= 624-draw resets in-wave (wave_reset); 16x16
-// resets go straight to k_init_fix_lane (most need >= 624 draws)
-template <class CF>
-constexpr bool INIT_INLINE_FIX = CF::N <= 128;
-constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
-
-// Per-shape step-kernel geometry: boards (lanes) per workgroup and the
-// match-group table capacity, sized so staging + table fit the 160 KB LDS.
-// One wave per workgroup: the boards of a wave are staged through its own LDS
-// slice, so a wave that finishes early never waits at a barrier for the
-// workgroup's slowest wave (cascade depth varies a lot between boards) and its
-// slot is refilled at once.
-template <class CF>
-struct KS {
-    static constexpr int B = 64;
-    static constexpr int GCAP = 4;                  // match groups in LDS (more spill to a global pool)
-#ifndef M3_STEP_WPS
-#define M3_STEP_WPS 4
+#ifdef M3_SPLIT_TU  // the launchers are instantiated in m3_inst.hip, one TU per configuration
+namespace m3k {
+M3_INSTANTIATE(extern template, CF_0)
+M3_INSTANTIATE(extern template, CF_1)
+M3_INSTANTIATE(extern template, CF_2)
+M3_INSTANTIATE(extern template, CF_3)
+M3_INSTANTIATE(extern template, CF_4)
+}  // namespace m3k
 #endif
-    // k_env_step waves per SIMD the register allocation is bounded for (16x16:
-    // 2, with 708 B of spill, +7 % over 1 once resets stopped binding)
-#ifndef M3_STEP_WPS16
-#define M3_STEP_WPS16 2
-#endif
-    static constexpr int STEP_WPS = CF::N > 128 ? M3_STEP_WPS16 : M3_STEP_WPS;
-    // k_env_cont: bounded like the step kernel it runs beside (a 2-waves/SIMD
-    // build without spills measured 4 % slower overall: its waves take register
-    // file the other shard's step waves need)
-#ifndef M3_CONT_WPS
-#define M3_CONT_WPS M3_STEP_WPS
-#endif
-    static constexpr int CONT_WPS = CF::N > 128 ? 1 : M3_CONT_WPS;
-    static constexpr uint32_t SPILL_RECORDS = 4096;  // spill pool records per shard
-    // The env step's RNG is the register-only MT19937 chain from the board's
-    // (seed, mt[397]) -- 4 B of per-board state (a per-board stream cache of
-    // the first raw outputs, built by the reset, measured equal at 9x9 and 2x
-    // slower at 16x16; removed in round 3).
-    // 16x16: one chain level (draws < 227; a step needing more -- a near-full
-    // board refill -- goes to k_env_fix), five fewer VGPRs live through the
-    // cascade, +2.5 %. 9x9: the full three-level chain; the one-level build
-    // came out 16 % slower (A/B gpurun_out/ab3), the register allocation of
-    // the 3-waves/SIMD bound shifts with it.
-    using Chain = std::conditional_t<(CF::N > 128), ChainMT1, ChainMT>;
-    using Rng = Chain;
-#ifndef M3_CASCADE_LIMIT
-#define M3_CASCADE_LIMIT 2
-#endif
-    // k_env_step runs at most this many cascade iterations per step (-1: no
-    // bound); longer steps are finished by k_env_cont (see there)
-    // (16x16: off -- the continuation launch cost more than it saved:
-    // 0.364 vs 0.337 G env-steps/s at 1 wave/SIMD, 0.391 vs 0.384 at 2)
-#ifndef M3_CASCADE_LIMIT16
-#define M3_CASCADE_LIMIT16 -1
-#endif
-    static constexpr int CASCADE_LIMIT = CF::N > 128 ? M3_CASCADE_LIMIT16 : M3_CASCADE_LIMIT;
-};
-
-// Per-lane match-group table (see m3_rules.hpp, match_scan): the first CAP
-// groups in LDS, entry (g, h|v, word i) of lane l at tab[((g*2 + hv)*W + i)*LANES + l]
-// (consecutive lanes hit consecutive dwords: conflict-free). A board that
-// forms more groups in one scan (~1e-3 of steps at CAP 4) takes a record from
-// a small global spill pool for groups CAP..MAXG-1; only a full pool (never in
-// practice) sends the step to the exact recompute pass.
-// LDS-only table (stateless kernels: a board with more groups is recomputed by k_apply_fix)
-template <class CF, int CAP_, int LANES>
-struct LdsTable {
-    static constexpr int CAP = CAP_;
-    static constexpr int W = CF::W;
-    static constexpr int BLOCK = LANES;
-    static constexpr int WORDS = CAP * 2 * W * BLOCK;
-    uint32_t* tab;  // already offset by threadIdx.x
-    __device__ __forceinline__ typename CF::Bd get_h(int g) const {
-        typename CF::Bd r;
-#pragma unroll
-        for (int i = 0; i < W; ++i) r.w[i] = tab[((g * 2) * W + i) * BLOCK];
-        return r;
-    }
-    __device__ __forceinline__ typename CF::Bd get_v(int g) const {
-        typename CF::Bd r;
-#pragma unroll
-        for (int i = 0; i < W; ++i) r.w[i] = tab[((g * 2 + 1) * W + i) * BLOCK];
-        return r;
-    }
-    __device__ __forceinline__ bool put(int g, const typename CF::Bd& h, const typename CF::Bd& v) {
-#pragma unroll
-        for (int i = 0; i < W; ++i) {
-            tab[((g * 2) * W + i) * BLOCK] = h.w[i];
-            tab[((g * 2 + 1) * W + i) * BLOCK] = v.w[i];
-        }
-        return true;
-    }
-};
-
-template <class CF, int CAP_, int LANES>
-struct LdsStore {
-    static constexpr int CAP = CF::MAXG;     // logical capacity (spill included)
-    static constexpr int LCAP = CAP_;        // groups held in LDS
-    static constexpr int W = CF::W;
-    static constexpr int BLOCK = LANES;
-    static constexpr int WORDS = LCAP * 2 * W * BLOCK;
-    static constexpr int SPILL_WORDS = (CF::MAXG - LCAP) * 2 * W;  // per pool record
-    uint32_t* tab;        // already offset by threadIdx.x
-    uint32_t* spill;      // nullable: pool of records
-    uint32_t* pool_next;  // pool allocation counter
-    uint32_t pool_cap;
-    uint32_t rec = ~0u;   // this lane's record
-    __device__ __forceinline__ typename CF::Bd get(int g, int hv) const {
-        typename CF::Bd r;
-        if (g < LCAP) {
-#pragma unroll
-            for (int i = 0; i < W; ++i) r.w[i] = tab[((g * 2 + hv) * W + i) * BLOCK];
-        } else {
-            const uint32_t* p = spill + (size_t)rec * SPILL_WORDS + ((g - LCAP) * 2 + hv) * W;
-#pragma unroll
-            for (int i = 0; i < W; ++i) r.w[i] = p[i];
-        }
-        return r;
-    }
-    __device__ __forceinline__ typename CF::Bd get_h(int g) const { return get(g, 0); }
-    __device__ __forceinline__ typename CF::Bd get_v(int g) const { return get(g, 1); }
-    __device__ __forceinline__ bool put(int g, const typename CF::Bd& h, const typename CF::Bd& v) {
-        if (g < LCAP) {
-#pragma unroll
-            for (int i = 0; i < W; ++i) {
-                tab[((g * 2) * W + i) * BLOCK] = h.w[i];
-                tab[((g * 2 + 1) * W + i) * BLOCK] = v.w[i];
-            }
-            return true;
-        }
-        if (rec == ~0u) rec = atomicAdd(pool_next, 1u);
-        const bool ok = rec < pool_cap;
-        if (ok) {
-            uint32_t* p = spill + (size_t)rec * SPILL_WORDS + (g - LCAP) * 2 * W;
-#pragma unroll
-            for (int i = 0; i < W; ++i) {
-                p[i] = h.w[i];
-                p[W + i] = v.w[i];
-            }
-        }
-        return ok;
-    }
-};
-
-// Phase profiling (profiling build only, -DM3_PHASE_PROF; tools/phase_prof.py).
-// mark<K>() charges the wave's cycles since the previous mark to phase K; the
-// first active lane keeps the per-wave accumulators in LDS, so the split is
-// exact wave time even inside divergent loops.
-#ifdef M3_PHASE_PROF
-constexpr int PROF_SLOTS = PH_N + 2;  // phases, total cycles, waves
-__device__ unsigned long long g_prof[2][PROF_SLOTS];  // [0] k_env_step, [1] k_init
-template <class Base>
-struct Prof : Base {
-    static constexpr bool PROF = true;
-    unsigned long long* w;  // this wave's LDS slot: PH_N accumulators, last, start
-    template <int K>
-    __device__ __forceinline__ void mark() {
-        const unsigned long long now = clock64();
-        if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) {
-            w[K] += now - w[PH_N];
-            w[PH_N] = now;
-        }
-    }
-    __device__ __forceinline__ void begin() {
-        if (__lane_id() == 0) {
-            for (int k = 0; k < PH_N; ++k) w[k] = 0;
-            w[PH_N] = w[PH_N + 1] = clock64();
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    __device__ __forceinline__ void end(int which) {
-        mark<PH_STORE>();
-        __builtin_amdgcn_wave_barrier();
-        if (__lane_id() == 0) {
-            for (int k = 0; k < PH_N; ++k) atomicAdd(&g_prof[which][k], w[k]);
-            atomicAdd(&g_prof[which][PH_N], w[PH_N] - w[PH_N + 1]);
-            atomicAdd(&g_prof[which][PH_N + 1], 1ull);
-        }
-    }
-};
-#define M3_PROF_LDS(LANES) __shared__ unsigned long long prof_s[(LANES) / 64][PH_N + 2];
-#endif
-
-// ---------------------------------------------------------------------------
-// LDS staging
-// ---------------------------------------------------------------------------
-template <int N, int BLOCK>
-__device__ __forceinline__ void block_copy_in(const int8_t* __restrict__ g, uint8_t* lds, int nb) {
-    const int bytes = nb * N;
-    const int n16 = bytes >> 4;
-    const uint4* s4 = reinterpret_cast<const uint4*>(g);
-    uint4* d4 = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < n16; i += BLOCK) d4[i] = s4[i];
-    for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) lds[i] = (uint8_t)g[i];
-}
-
-template <int N, int BLOCK>
-__device__ __forceinline__ void block_copy_out(int8_t* __restrict__ g, const uint8_t* lds, int nb) {
-    const int bytes = nb * N;
-    const int n16 = bytes >> 4;
-    const uint4* s4 = reinterpret_cast<const uint4*>(lds);
-    uint4* d4 = reinterpret_cast<uint4*>(g);
-    for (int i = threadIdx.x; i < n16; i += BLOCK) d4[i] = s4[i];
-    for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) g[i] = (int8_t)lds[i];
-}
-
-// N cell bytes (little-endian in cw[ceil(N/4)]) to dst of any alignment:
-// up to 3 head bytes, aligned dwords (one funnel shift each), up to 3 tail
-// bytes -- instead of N byte stores.
-template <int N>
-__device__ __forceinline__ void store_cells(uint8_t* dst, const uint32_t* cw) {
-    constexpr int NW = (N + 3) / 4;
-    const uint32_t head = (4u - ((uint32_t)(uintptr_t)dst & 3u)) & 3u;
-    const uint32_t nd = ((uint32_t)N - head) >> 2;
-    const uint32_t t0 = head + 4u * nd;
-    const uint32_t s = 8u * head;
-#pragma unroll
-    for (int y = 0; y < 3; ++y)
-        if ((uint32_t)y < head) dst[y] = (uint8_t)(cw[y >> 2] >> (8 * (y & 3)));
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-        if ((uint32_t)i < nd) {
-            const uint32_t lo = cw[i], hi = (i + 1 < NW) ? cw[i + 1] : 0u;
-            d32[i] = s ? ((lo >> s) | (hi << (32u - s))) : lo;
-        }
-    }
-#pragma unroll
-    for (int y = N - 3; y < N; ++y)
-        if ((uint32_t)y >= t0) dst[y] = (uint8_t)(cw[y >> 2] >> (8 * (y & 3)));
-}
-
-// lane's board (N bytes at lds + slot*N, any alignment) -> bit-planes.
-// The dword window may reach into the neighbour's bytes; planes_from_words
-// masks every bit >= N.
-template <class CF>
-__device__ __forceinline__ void lds_to_planes(const uint8_t* lds, int slot, typename CF::Bd* P) {
-    constexpr int NW = (CF::N + 3) / 4;
-    const int off = slot * CF::N;
-    const uint32_t* d = reinterpret_cast<const uint32_t*>(lds + (off & ~3));
-    const uint32_t sh = (uint32_t)(off & 3) * 8u;
-    uint32_t cw[NW];
-    uint32_t prev = d[0];
-#pragma unroll
-    for (int q = 0; q < NW; ++q) {
-        const uint32_t next = d[q + 1];
-        cw[q] = __builtin_amdgcn_alignbit(next, prev, sh);
-        prev = next;
-    }
-    planes_from_words<CF>(cw, P);
-}
-
-template <class CF>
-__device__ __forceinline__ void planes_to_bytes(const typename CF::Bd* P, uint8_t* dst) {
-    constexpr int NW = (CF::N + 3) / 4;
-    uint32_t cw[NW];
-    words_from_planes<CF>(P, cw);
-    store_cells<CF::N>(dst, cw);
-}
-
-template <class CF>
-__device__ __forceinline__ void bytes_to_planes(const int8_t* src, typename CF::Bd* P) {
-    constexpr int NW = (CF::N + 3) / 4;
-    uint32_t cw[NW];
-#pragma unroll
-    for (int q = 0; q < NW; ++q) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int x = 4 * q + k;
-            if (x < CF::N) v |= (uint32_t)(uint8_t)src[x] << (8 * k);
-        }
-        cw[q] = v;
-    }
-    planes_from_words<CF>(cw, P);
-}
-
-template <class CF>
-__device__ __forceinline__ void store_legal(uint32_t* out, const uint32_t* act) {
-#pragma unroll
-    for (int i = 0; i < CF::AW; ++i) out[i] = act[i];
-}
-
-// ---------------------------------------------------------------------------
-// stateless kernels (BoardV2 facade): m3_apply_actions / m3_init_boards /
-// m3_legal_actions
-// ---------------------------------------------------------------------------
-struct ApplyArgs {
-    int64_t n;
-    const int8_t* boards;
-    const uint32_t* seeds;
-    const int32_t* n_actions;
-    const int32_t* actions;
-    int8_t* out_boards;
-    int32_t* reward;
-    uint32_t* draws;
-    uint32_t* flags;
-    uint32_t* legal;       // nullable
-    int32_t* next_action;  // nullable
-    uint32_t* ovf_count;
-    uint32_t* ovf_list;
-};
-
-// one full apply_action + outputs for board b; returns false on RNG overflow
-template <class CF, class RNG, class Store>
-__device__ __forceinline__ bool apply_and_emit(typename CF::Bd* P, const ApplyArgs& a, int64_t b, RNG& rng,
-                                               Store& st) {
-    typename CF::Bd HL, VL;
-    uint32_t f;
-    const int r = apply_action<CF>(P, a.n_actions[b], a.actions[b], rng, f, HL, VL, st);
-    if (f & FLAG_RECOMPUTE) return false;
-    const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
-    a.reward[b] = r;
-    a.draws[b] = stepped ? rng.draws() : 0u;
-    uint32_t act[CF::AW];
-    action_bits<CF>(HL, VL, act);
-    int na = -1;
-    if (stepped) {
-        na = random_action<CF>(act, rng);
-        if (rng.overflow) return false;
-        if (na < 0) f |= FLAG_NO_LEGAL;
-    }
-    mark<PH_NEXT>(st);
-    a.flags[b] = f;
-    if (a.next_action) a.next_action[b] = na;
-    if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
-    return true;
-}
-
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B) k_apply(ApplyArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[KS<CF>::B * CF::N + 16];
-    __shared__ uint32_t gtab[LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::WORDS];
-    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
-    const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
-    block_copy_in<CF::N, KS<CF>::B>(a.boards + b0 * CF::N, lds, nb);
-    __syncthreads();
-    const int t = threadIdx.x;
-    if (t < nb) {
-        const int64_t b = b0 + t;
-        typename CF::Bd P[CF::NP];
-        lds_to_planes<CF>(lds, t, P);
-        const uint32_t s = a.seeds[b];
-        ChainMT rng;
-        rng.init(s, mt_state397(s));
-        LdsTable<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};  // overflow -> k_apply_fix
-        if (!apply_and_emit<CF>(P, a, b, rng, st)) {
-            const uint32_t slot = atomicAdd(a.ovf_count, 1u);
-            a.ovf_list[slot] = (uint32_t)b;
-        }
-        planes_to_bytes<CF>(P, lds + t * CF::N);
-    }
-    __syncthreads();
-    block_copy_out<CF::N, KS<CF>::B>(a.out_boards + b0 * CF::N, lds, nb);
-}
-
-// redo overflowed boards with the full 624-word state (lane-private scratch)
-template <class CF>
-__global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
-    const uint32_t cnt = *a.ovf_count;
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
-        const int64_t b = a.ovf_list[i];
-        typename CF::Bd P[CF::NP];
-        bytes_to_planes<CF>(a.boards + b * CF::N, P);
-        FullMT mt;  // scratch: this pass almost never has work, and an LDS state would
-                    // make even an empty launch wait for a whole free CU
-        mt.init(a.seeds[b], 0u);
-        ArrayStore<CF> st;
-        apply_and_emit<CF>(P, a, b, mt, st);
-        uint8_t tmp[CF::N];
-        planes_to_bytes<CF>(P, tmp);
-        for (int x = 0; x < CF::N; ++x) a.out_boards[b * CF::N + x] = (int8_t)tmp[x];
-    }
-}
-
-constexpr int NSLOT = 4;            // episode slots per board (see EnvArgs)
-constexpr int PF_LAG = NSLOT - 1;   // steps between a prefetch and its first use
-
-// A reset launch processes "items". Item i is (board b, seed, slot): with a
-// list (env prefetch) b = list[i], seed = list_seed[i], slot = list_slot[i];
-// without, b = i, seed = seeds[i] + seed_add, slot = slot_of ? (slot_of[b] +
-// slot0) % NSLOT : slot0. Per-board outputs go to index ob = slot * sstride + b
-// (sstride 0 = the env's current state, n = one of the episode slots).
-struct InitArgs {
-    int64_t n;
-    const uint32_t* list;        // nullable
-    const uint32_t* list_seed;
-    const uint32_t* list_slot;
-    const uint32_t* list_count;  // device count for list
-    const uint32_t* seeds;       // implicit items
-    uint32_t seed_add;
-    uint32_t slot0;
-    const uint8_t* slot_of;      // nullable
-    int64_t sstride;
-    int8_t* boards;              // cells as bytes at ob * N            (one of boards /
-    uint32_t* board_words;       // cells as LE words at ob * NW         board_words)
-    uint32_t* draws;             // nullable
-    int32_t* first_action;       // nullable
-    uint32_t* legal;             // nullable
-    int32_t* score;              // nullable: zeroed episode state (explicit env reset)
-    int32_t* moves;
-    int32_t* reward;
-    uint8_t* done;
-    uint8_t* trunc;
-    uint32_t* flags;
-    uint32_t* stats;             // nullable: [0] resets, [1] reset recomputes (>= 624 draws)
-    uint32_t* m397;              // nullable: mt[397] of the seed's init_genrand state at (slot, b)
-    int64_t cstride;
-};
-
-__device__ __forceinline__ void init_item(const InitArgs& a, int64_t i, int64_t& b, uint32_t& seed, uint32_t& slot) {
-    if (a.list) {
-        b = (int64_t)a.list[i];
-        seed = a.list_seed[i];
-        slot = a.list_slot[i];
-    } else {
-        b = i;
-        seed = a.seeds[b] + a.seed_add;
-        slot = a.slot_of ? ((uint32_t)a.slot_of[b] + a.slot0) % (uint32_t)NSLOT : a.slot0;
-    }
-}
-
-template <class CF>
-__device__ __forceinline__ void init_store_board(const InitArgs& a, int64_t ob, const uint32_t* cw) {
-    constexpr int NW = (CF::N + 3) / 4;
-    if (a.board_words) {
-#pragma unroll
-        for (int q = 0; q < NW; ++q) a.board_words[ob * NW + q] = cw[q];
-    } else {
-        store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.boards + ob * CF::N), cw);
-    }
-}
-
-// BoardV2.__init__ (boardv2.py:17-27) + first seeded random action
-// (samplerTasks.py:11-13) for board b. Returns false if the stream overflowed.
-// Everything a reset writes besides the cells: legal set, the first seeded
-// random action (np.random.seed(cfg.seed) then choice(legal), samplerTasks.py:11-13),
-// the cached mt[397] and the zeroed episode state.
-template <class CF>
-__device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, int64_t ob, uint32_t seed, uint32_t m397,
-                                             uint32_t draws, const typename CF::Bd* P) {
-    typename CF::Bd HL, VL;
-    legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
-    uint32_t act[CF::AW];
-    action_bits<CF>(HL, VL, act);
-    ChainMT rng;
-    rng.init(seed, m397);
-    const int fa = random_action<CF>(act, rng);
-    if (a.draws) a.draws[ob] = draws;
-    if (a.first_action) a.first_action[ob] = fa;
-    if (a.legal) store_legal<CF>(a.legal + ob * CF::AW, act);
-    if (a.score) a.score[b] = 0;
-    if (a.moves) a.moves[b] = 0;
-    if (a.reward) a.reward[b] = 0;
-    if (a.done) a.done[b] = 0;
-    if (a.trunc) a.trunc[b] = 0;
-    if (a.flags) a.flags[b] = fa < 0 ? FLAG_NO_LEGAL : 0u;
-}
-
-// Reset of board b on a tile stream generated in LDS (init_board_tiles).
-// Returns false if the reset needs >= 624 draws (wave_reset / k_init_fix redo it).
-template <class CF, class S = NoStore>
-__device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t slot, uint32_t m397,
-                                          uint32_t* tm, uint32_t* pos, S* ps = nullptr) {
-    typename CF::Bd P[CF::NP];
-    ChainMT g;
-    g.init(seed, m397);
-    if (a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;
-    uint32_t draws = 0;
-    const bool ok = init_board_tiles<CF>(
-        P, g, tm, pos, INIT_BLOCK, draws, 0u, [](uint32_t, uint32_t) {}, [](uint32_t, uint32_t) {}, ps);
-    if (!ok) return false;
-    const int64_t ob = (int64_t)slot * a.sstride + b;
-    init_outputs<CF>(a, b, ob, seed, m397, draws, P);
-    constexpr int NW = (CF::N + 3) / 4;
-    uint32_t cw[NW];
-    words_from_planes<CF>(P, cw);
-    init_store_board<CF>(a, ob, cw);
-    return true;
-}
-
-// ---- wave-cooperative reset for boards whose reset needs >= 624 draws ----
-// One board per wave. The 624-word MT19937 state sits in LDS; the twist runs
-// on all 64 lanes (three dependency phases), and randint(1, T+1) over the
-// board is a parallel filter: 64 raw outputs per trip, ballot of the accepted
-// ones, prefix popcount for their cell. The bitboard logic (get_matches
-// mask, legal, first action) runs redundantly on every lane, so control flow
-// stays wave-uniform. Latency ~tens of us instead of ~1 ms for one lane
-// walking the state.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ void wave_twist(uint32_t* key, int lane) {  // numpy mt19937_gen
-    for (int base = 0; base < 227; base += 64) {  // mt'[i] = mt[i+397] ^ twist(mt[i], mt[i+1])
-        const int i = base + lane;
-        uint32_t a0 = 0, a1 = 0, x = 0;
-        if (i < 227) { a0 = key[i]; a1 = key[i + 1]; x = key[i + 397]; }
-        asm volatile("" ::: "memory");  // every lane's loads before any lane's store
-        if (i < 227) key[i] = x ^ mt_twist(a0, a1);
-        wave_sync();
-    }
-    for (int base = 227; base < 623; base += 64) {  // mt'[i] = mt'[i-227] ^ twist(mt[i], mt[i+1])
-        const int i = base + lane;
-        uint32_t a0 = 0, a1 = 0, x = 0;
-        if (i < 623) { a0 = key[i]; a1 = key[i + 1]; x = key[i - 227]; }
-        asm volatile("" ::: "memory");
-        if (i < 623) key[i] = x ^ mt_twist(a0, a1);
-        wave_sync();
-    }
-    if (lane == 0) key[623] = key[396] ^ mt_twist(key[623], key[0]);
-    wave_sync();
-}
-
-__device__ __forceinline__ int select_bit64(uint64_t m, int k) {
-    const uint32_t lo = (uint32_t)m;
-    const int c = __builtin_popcount(lo);
-    return k < c ? select_bit(lo, k) : 32 + select_bit((uint32_t)(m >> 32), k - c);
-}
-
-// RandomState.randint(1, T+1, (R, C)) into cells (only where `only` is set,
-// if given); advances (pos, k) over the LDS state exactly as numpy would.
-template <class CF>
-__device__ __forceinline__ void wave_fill(uint32_t* key, uint8_t* cells, int lane, uint32_t& pos, uint32_t& k,
-                                          const typename CF::Bd* only) {
-    int filled = 0;
-    while (filled < CF::N) {
-        if constexpr (CF::TILE_RNG == 0u) {  // randint(1, 2): no draws consumed
-            for (int c = lane; c < CF::N; c += 64)
-                if (!only || only->test(c)) cells[c] = 1;
-            break;
-        }
-        if (pos == 624u) {
-            wave_twist(key, lane);
-            pos = 0u;
-        }
-        const int take = (int)min(64u, 624u - pos);
-        uint32_t v = 0;
-        bool acc = false;
-        if (lane < take) {
-            v = mt_temper(key[pos + lane]) & CF::TILE_MASK;
-            acc = v <= CF::TILE_RNG;
-        }
-        const uint64_t bal = __ballot(acc);
-        const int rank = __builtin_popcountll(bal & ((1ull << lane) - 1ull));
-        const int need = CF::N - filled, got = __builtin_popcountll(bal);
-        if (acc && rank < need) {
-            const int c = filled + rank;
-            if (!only || only->test(c)) cells[c] = (uint8_t)(v + 1u);
-        }
-        const int used = got >= need ? select_bit64(bal, need - 1) + 1 : take;
-        pos += (uint32_t)used;
-        k += (uint32_t)used;
-        filled += got >= need ? need : got;
-    }
-    wave_sync();
-}
-
-// One reset (item of the launch) by the whole wave; key: 624 words of LDS, cells: N bytes of LDS.
-template <class CF>
-__device__ void wave_reset(const InitArgs& a, int64_t item, uint32_t* key, uint8_t* cells, int lane) {
-    int64_t b;
-    uint32_t seed, slot;
-    init_item(a, item, b, seed, slot);
-    if (lane == 0) {  // init_genrand is a serial recurrence
-        uint32_t x = seed;
-        for (uint32_t p = 0; p < 624u; ++p) {
-            key[p] = x;
-            x = mt_init_next(x, p + 1u);
-        }
-    }
-    wave_sync();
-    const uint32_t m397 = key[397];
-    uint32_t pos = 624u, k = 0u;
-    wave_fill<CF>(key, cells, lane, pos, k, nullptr);                  // boardv2.py:21
-    typename CF::Bd P[CF::NP], mask;
-    planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
-    while (get_match_mask<CF>(P, mask)) {                               // boardv2.py:23-27
-        wave_fill<CF>(key, cells, lane, pos, k, &mask);
-        planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
-    }
-    const int64_t ob = (int64_t)slot * a.sstride + b;
-    if (lane == 0) init_outputs<CF>(a, b, ob, seed, m397, k, P);
-    if (a.board_words) {
-        for (int q = lane; q < (CF::N + 3) / 4; q += 64)
-            a.board_words[ob * ((CF::N + 3) / 4) + q] = reinterpret_cast<const uint32_t*>(cells)[q];
-    } else {
-        int8_t* dst = a.boards + ob * CF::N;
-        for (int x = lane; x < CF::N; x += 64) dst[x] = (int8_t)cells[x];
-    }
-    wave_sync();
-}
-
-// Reset on the register-only MT19937 chain; grid-strided over n (or *list_count).
-// A reset that needs >= 624 draws (~0.7 % at 9x9x6) is redone by its own wave
-// right away (wave_reset).
-template <class CF>
-__global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
-    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
-    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.stats[0], (uint32_t)cnt);
-    __shared__ uint32_t tm_s[CF::BITS * TileGen<CF>::TWMAX * INIT_BLOCK];
-    __shared__ uint32_t pos_s[TileGen<CF>::MAXR * INIT_BLOCK];
-    uint32_t* tm = tm_s + threadIdx.x;
-    uint32_t* pos = pos_s + threadIdx.x;
-#ifdef M3_PHASE_PROF
-    M3_PROF_LDS(INIT_BLOCK)
-    Prof<NoStore> ps;
-    ps.w = prof_s[threadIdx.x >> 6];
-    const bool live = (int64_t)blockIdx.x * INIT_BLOCK < cnt;
-    if (live) ps.begin();
-#else
-    NoStore* const pp = nullptr;
-#endif
-    static_assert(INIT_INLINE_FIX<CF> && INIT_BLOCK == 64, "the in-wave redo is one wave's");
-    __shared__ uint32_t key_s[624];
-    __shared__ __attribute__((aligned(16))) uint8_t cell_s[(CF::N + 3) / 4 * 4 + 16];
-    for (int64_t base = (int64_t)blockIdx.x * INIT_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_BLOCK) {
-        const int64_t i = base + threadIdx.x;
-        bool ok = true;
-        if (i < cnt) {
-            int64_t b;
-            uint32_t seed, slot;
-            init_item(a, i, b, seed, slot);
-            const uint32_t m397 = mt_state397(seed);
-#ifdef M3_PHASE_PROF
-            ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, &ps);
-#else
-            ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, pp);
-#endif
-        }
-        // this wave redoes its >= 624-draw resets at once
-        uint64_t bad = __ballot(!ok);
-        if (bad && a.stats && threadIdx.x == 0) atomicAdd(&a.stats[1], (uint32_t)__builtin_popcountll(bad));
-        while (bad) {
-            const int l = __builtin_ctzll(bad);
-            bad &= bad - 1ull;
-            wave_reset<CF>(a, __shfl(i, l), key_s, cell_s, (int)threadIdx.x);
-        }
-    }
-#ifdef M3_PHASE_PROF
-    if (live) ps.end(1);
-#endif
-}
-
-// ---- lane-per-board reset for boards that need >= 624 draws -------------
-// One board per lane with the full 624-word MT19937 state in lane-private
-// scratch (FullMT; scratch is swizzled per lane, so the state accesses of a
-// wave are coalesced). At 9x9x6 ~0.7% of resets land here, at 16x16x8 ~60%
-// (every round of randint(1, 9, (16, 16)) takes 256 draws), so this pass is
-// throughput work: all 64 lanes of a wave run their own board.
-//
-// One round of BoardV2.__init__ (boardv2.py:21 / :25): randint(1, T+1, (R, C))
-// draws a tile for EVERY cell in row-major order; cells outside `only` take
-// their draw and drop it (array[mask] = new[mask]). A plane word collects 32
-// tiles, then merges under the mask.
-template <class CF, class RNG>
-__device__ __forceinline__ void fill_round(typename CF::Bd* P, RNG& mt, const typename CF::Bd* only) {
-#pragma unroll
-    for (int w = 0; w < CF::W; ++w) {
-        constexpr int BITS = CF::BITS;
-        const int nbits = CF::N - 32 * w < 32 ? CF::N - 32 * w : 32;
-        uint32_t t[BITS];
-#pragma unroll
-        for (int p = 0; p < BITS; ++p) t[p] = 0u;
-        int bit = 0;
-        if constexpr (CF::TILE_RNG != 0u && CF::TILE_RNG == CF::TILE_MASK) {
-            // T a power of two: every draw is a tile, so a word is nbits consecutive outputs
-            if (mt.bulk_ready((uint32_t)nbits)) {
-#pragma unroll
-                for (int j = 0; j < nbits; ++j) {
-                    const uint32_t v = (mt.bulk_out((uint32_t)j) & CF::TILE_MASK) + 1u;
-#pragma unroll
-                    for (int p = 0; p < BITS; ++p) t[p] |= ((v >> p) & 1u) << j;
-                }
-                mt.bulk_skip((uint32_t)nbits);
-                bit = nbits;
-            }
-        }
-        for (; bit < nbits; ++bit) {
-            uint32_t v = 1u;
-            if constexpr (CF::TILE_RNG != 0u) {
-                do {
-                    v = mt.next32() & CF::TILE_MASK;
-                } while (v > CF::TILE_RNG);
-                v += 1u;
-            }
-#pragma unroll
-            for (int p = 0; p < BITS; ++p) t[p] |= ((v >> p) & 1u) << bit;
-        }
-        const uint32_t m = only ? only->w[w] : 0xFFFFFFFFu;
-#pragma unroll
-        for (int p = 0; p < BITS; ++p) P[p].w[w] = (P[p].w[w] & ~m) | (t[p] & m);
-    }
-}
-
-// Every reset of the launch (k_init is skipped at 16x16x8: most resets
-// overflow the chain anyway). stats[1] counts the resets that needed >= 624
-// draws, as k_init's in-wave redo does at 9x9, so the counter means the same
-// at both shapes.
-template <class CF>
-__global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
-    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
-    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], (uint32_t)cnt);
-    for (int64_t base = (int64_t)blockIdx.x * INIT_FIX_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_FIX_BLOCK) {
-        const int64_t oi = base + threadIdx.x;
-        bool long_reset = false;
-        if (oi < cnt) {
-            int64_t b;
-            uint32_t seed, slot;
-            init_item(a, oi, b, seed, slot);
-            FullMT mt;
-            mt.init(seed, 0u);
-            const uint32_t m397 = mt.key[397];  // init_genrand state, before the first twist
-            if (a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;
-            typename CF::Bd P[CF::NP], mask;
-#pragma unroll
-            for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
-            fill_round<CF>(P, mt, nullptr);                              // boardv2.py:21
-            while (get_match_mask<CF>(P, mask)) fill_round<CF>(P, mt, &mask);  // boardv2.py:23-27
-            const int64_t ob = (int64_t)slot * a.sstride + b;
-            init_outputs<CF>(a, b, ob, seed, m397, mt.draws(), P);
-            constexpr int NW = (CF::N + 3) / 4;
-            uint32_t cw[NW];
-            words_from_planes<CF>(P, cw);
-            init_store_board<CF>(a, ob, cw);
-            long_reset = mt.draws() >= 624u;
-        }
-        const uint64_t m = __ballot(long_reset);
-        if (m && a.stats && (threadIdx.x & 63) == 0) atomicAdd(&a.stats[1], (uint32_t)__popcll(m));
-    }
-}
-
-// mt[397] of init_genrand(seeds[b]): the chain word of each board's current
-// episode (env resume, m3_env_set)
-__global__ void __launch_bounds__(256) k_mt397(int64_t n, const uint32_t* seeds, uint32_t* out) {
-    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < n; b += (int64_t)gridDim.x * 256)
-        out[b] = mt_state397(seeds[b]);
-}
-
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B) k_legal(int64_t n, const int8_t* boards, uint32_t* legal) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[KS<CF>::B * CF::N + 16];
-    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
-    const int nb = (int)((n - b0) < KS<CF>::B ? (n - b0) : KS<CF>::B);
-    block_copy_in<CF::N, KS<CF>::B>(boards + b0 * CF::N, lds, nb);
-    __syncthreads();
-    const int t = threadIdx.x;
-    if (t < nb) {
-        typename CF::Bd P[CF::NP], HL, VL;
-        lds_to_planes<CF>(lds, t, P);
-        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
-        uint32_t act[CF::AW];
-        action_bits<CF>(HL, VL, act);
-        store_legal<CF>(legal + (b0 + t) * CF::AW, act);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// batched env (n x Match3Env, env.py:8-65)
-// ---------------------------------------------------------------------------
-// Autoreset keeps NSLOT episode slots per board: the current episode's stream
-// cache is slot cur[b]; slots cur+1 .. cur+NSLOT-1 hold the next episodes
-// (seed + k*stride) -- initial board, first action, legal set and stream
-// cache -- computed ahead by the prefetch pass (k_init on its own stream). A
-// finished board swaps in slot cur+1 inside the step and queues slot cur (now
-// free) for the episode NSLOT-1 ahead; the prefetch of step t is only needed
-// NSLOT-1 steps later, so resets never sit on the step's critical path.
-
-struct EnvArgs {
-    int64_t n;
-    int num_moves, goal;
-    int autoreset;
-    uint32_t stride;         // autoreset seed increment
-    const int8_t* cur;
-    int8_t* nxt;
-    const int32_t* actions;  // nullable -> next_action
-    uint32_t* seeds;
-    int32_t* score;
-    int32_t* moves;
-    int32_t* next_action;
-    int32_t* reward;
-    uint8_t* done;
-    uint8_t* trunc;
-    uint32_t* flags;
-    uint32_t* draws;
-    uint32_t* legal;  // nullable
-    int32_t* packed;  // nullable: reward<<2 | trunc<<1 | done for the RCCL gather
-    uint32_t* counters;  // this step's block: [0] overflow count, [1] prefetch count, [2] prefetch overflow
-                         // count, [3] spill records used, [4] continuation records
-    uint32_t* spill;     // group-table spill pool of the shard
-    uint32_t* stats;     // [0] step recomputes
-    uint32_t* ovf_list;
-    uint8_t* slot;       // current episode slot per board
-    const uint32_t* ne_words;  // episode slots: initial cells (LE words) [3][n][NW]
-    const int32_t* ne_first;   // [3][n] first seeded random action
-    const uint32_t* ne_legal;  // [3][n][AW]
-    uint32_t* pf_list;   // prefetch queue of this step: board, seed, slot
-    uint32_t* pf_seed;
-    uint32_t* pf_slot;
-    const uint32_t* m397;  // [NSLOT][cstride] mt[397] of each slot's seed
-    int64_t cstride;
-    uint32_t* cont;        // nullable: continuation records of paused steps (k_env_cont), [1 + WORDS][cont_stride]
-    int64_t cont_stride;
-};
-
-// Match3Env.step bookkeeping (env.py:48-56) after BoardV2.apply_action (r, f,
-// HL/VL of the resulting board), and the same-step autoreset (the finished
-// step's reward/done/flags stay visible, the observation and episode state
-// become the next episode's). mv / sc0: the board's moves and score before the
-// step. Returns false if the next random action ran past the RNG (recompute).
-// board_src (nullable): instead of loading the next episode's cells into P,
-// report their word row ob (ne_words[ob * NW ...]; -1 without a reset) so the
-// caller copies them once P is dead (k_env_step: keeps its register peak low).
-template <class CF, class RNG, class Store>
-__device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
-                                           int r, uint32_t f, const typename CF::Bd& HL, const typename CF::Bd& VL,
-                                           int mv, int sc0, int64_t* board_src = nullptr) {
-    const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
-    const int sc = sc0 + r;
-    const int mv1 = mv + 1;
-    const int tr = sc >= a.goal;                        // env.py:53
-    const int dn = tr || mv1 == a.num_moves;            // env.py:54
-    a.draws[b] = stepped ? rng.draws() : 0u;
-    uint32_t act[CF::AW];
-    action_bits<CF>(HL, VL, act);
-    int na = -1;
-    if (stepped) {
-        na = random_action<CF>(act, rng);
-        if (rng.overflow) return false;
-        if (na < 0) f |= FLAG_NO_LEGAL;
-    }
-    mark<PH_NEXT>(st);
-    a.reward[b] = r;
-    a.trunc[b] = (uint8_t)tr;
-    a.done[b] = (uint8_t)dn;
-    a.flags[b] = f;
-    if (a.packed) a.packed[b] = (r << 2) | (tr << 1) | dn;
-    const bool reset = dn && a.autoreset;
-    if (!reset) {
-        a.score[b] = sc;
-        a.moves[b] = mv1;
-        a.next_action[b] = na;
-        if (a.legal) store_legal<CF>(a.legal + b * CF::AW, act);
-    } else {  // swap in the prefetched next episode (slot + 1)
-        constexpr int NW = (CF::N + 3) / 4;
-        const uint32_t s_old = a.slot[b], s_new = s_old + 1u == (uint32_t)NSLOT ? 0u : s_old + 1u;
-        const int64_t ob = (int64_t)s_new * a.cstride + b;  // slots are strided by the env's n
-        const uint32_t seed = a.seeds[b] + a.stride;
-        if (board_src) {
-            *board_src = ob;
-        } else {
-            uint32_t cw[NW];
-#pragma unroll
-            for (int q = 0; q < NW; ++q) cw[q] = a.ne_words[ob * NW + q];
-            planes_from_words<CF>(cw, P);
-        }
-        a.slot[b] = (uint8_t)s_new;
-        a.seeds[b] = seed;
-        a.score[b] = 0;
-        a.moves[b] = 0;
-        a.next_action[b] = a.ne_first[ob];
-        if (a.legal) {
-#pragma unroll
-            for (int i = 0; i < CF::AW; ++i) a.legal[b * CF::AW + i] = a.ne_legal[ob * CF::AW + i];
-        }
-    }
-    mark<PH_RESET>(st);
-    // queue the freed slot for the episode after next: one atomic per wave, not per lane
-    const uint64_t m = __ballot(reset);
-    if (m) {
-        const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&a.counters[1], (uint32_t)__popcll(m));
-        base = __shfl(base, leader);
-        if (reset) {
-            const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            a.pf_list[q] = (uint32_t)b;
-            a.pf_seed[q] = a.seeds[b] + (uint32_t)(NSLOT - 1) * a.stride;
-            a.pf_slot[q] = a.slot[b] == 0u ? (uint32_t)(NSLOT - 1) : a.slot[b] - 1u;
-        }
-    }
-    mark<PH_QUEUE>(st);
-    return true;
-}
-
-enum : int { ENV_STEP_DONE = 0, ENV_STEP_RECOMPUTE = 1, ENV_STEP_PAUSED = 2 };
-
-// internal: a continuation record of a settled board with no legal move (the
-// row shuffle comes next), as opposed to one paused before a cascade iteration
-constexpr uint32_t FLAG_CONT_DEAD = 0x80u;
-
-// One Match3Env.step of board b. With DEFER (k_env_step), the cascade stops
-// after `limit` inner iterations and at a dead board (the shuffle path is left
-// out of the kernel): the step returns ENV_STEP_PAUSED with its state in P,
-// rng, r, f (f & FLAG_CONT_DEAD: dead) and has written nothing yet; k_env_cont
-// finishes it. Without DEFER the whole step runs here.
-template <class CF, bool DEFER, class RNG, class Store>
-__device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
-                                            int limit, int& r, uint32_t& f, int64_t* board_src = nullptr) {
-    // every per-board input is loaded before the cascade, so its latency hides behind it
-    const int act_in = a.actions ? a.actions[b] : a.next_action[b];
-    const int mv = a.moves[b];
-    const int sc0 = a.score[b];
-    typename CF::Bd HL, VL;
-    if (apply_begin<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st, r)) {
-        const int c = apply_cascade_ex<CF, DEFER ? CASX_STOP_DEAD : 0>(P, rng, f, HL, VL, st, r, limit, false);
-        if (!(f & FLAG_RECOMPUTE)) {
-            if (c == CAS_PAUSED) return ENV_STEP_PAUSED;
-            if (c == CAS_DEAD) {
-                f |= FLAG_CONT_DEAD;
-                return ENV_STEP_PAUSED;
-            }
-        }
-    }
-    if (f & FLAG_RECOMPUTE) return ENV_STEP_RECOMPUTE;
-    return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, board_src) ? ENV_STEP_DONE : ENV_STEP_RECOMPUTE;
-}
-
-// Continuation records of paused steps (KS::CASCADE_LIMIT): word 0 the
-// shard-local board index, words 1.. the Cont state; word w of record q at
-// cont[w * cont_stride + q] (consecutive records of a wave are consecutive
-// dwords). cont_count (the step's counter block [4]) counts them.
-template <class CF>
-using EnvCont = Cont<CF, typename KS<CF>::Rng>;
-
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArgs a) {
-    // The board staging area is only live before the cascade (HBM -> LDS ->
-    // planes) and after it (planes -> LDS -> HBM), the match-group table only
-    // inside it; with one wave per workgroup nothing else can touch the LDS
-    // in between, so the two share storage (13.3 KB per wave at 9x9: 3 waves/SIMD).
-    using K = KS<CF>;
-    static_assert(K::B == 64, "staging/table aliasing assumes one wave per workgroup");
-    constexpr int STAGE_WORDS = (K::B * CF::N + 16 + 3) / 4;
-    constexpr int TAB_WORDS = LdsStore<CF, K::GCAP, K::B>::WORDS;
-    __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
-    uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
-    uint32_t* const gtab = stage_tab;
-    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
-    const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
-    block_copy_in<CF::N, KS<CF>::B>(a.cur + b0 * CF::N, lds, nb);
-    const int t = threadIdx.x;
-    const uint32_t cslot = t < nb ? a.slot[b0 + t] : 0u;
-    __syncthreads();
-#ifdef M3_PHASE_PROF
-    M3_PROF_LDS(KS<CF>::B)
-    Prof<LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>> st;
-    st.tab = gtab + t;
-    st.w = prof_s[t >> 6];
-    const bool live = ((t & ~63) < nb);
-    if (live) st.begin();
-#else
-    LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};
-#endif
-    st.spill = a.spill;
-    st.pool_next = &a.counters[3];
-    st.pool_cap = K::SPILL_RECORDS;
-    if (t < nb) {
-        const int64_t b = b0 + t;
-        typename CF::Bd P[CF::NP];
-        lds_to_planes<CF>(lds, t, P);
-        typename K::Rng rng;
-        rng.init(a.seeds[b], a.m397[(int64_t)cslot * a.cstride + b]);
-        int r;
-        uint32_t f;
-        int res;
-        int64_t reset_src = -1;  // autoreset: the next episode's cells, copied below once P is dead
-        if constexpr (K::CASCADE_LIMIT >= 0)  // (a.cont is set)
-            res = env_step_one<CF, true>(P, a, b, rng, st, K::CASCADE_LIMIT, r, f, &reset_src);
-        else
-            res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f, &reset_src);
-        if (res == ENV_STEP_RECOMPUTE) {
-            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-            a.ovf_list[slot] = (uint32_t)b;
-        }
-        // paused steps leave a continuation record (one atomic per wave)
-        const bool paused = res == ENV_STEP_PAUSED;
-        const uint64_t m = __ballot(paused);
-        if (m) {
-            const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            if (paused) {
-                const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                uint32_t* rec = a.cont + q;
-                const int64_t cs = a.cont_stride;
-                rec[0] = (uint32_t)b;
-                EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
-            }
-        }
-        planes_to_bytes<CF>(P, lds + t * CF::N);  // a paused board's bytes are rewritten by k_env_cont
-        if (reset_src >= 0) {
-            constexpr int NW = (CF::N + 3) / 4;
-            uint32_t cw[NW];
-#pragma unroll
-            for (int q = 0; q < NW; ++q) cw[q] = a.ne_words[reset_src * NW + q];
-            store_cells<CF::N>(lds + t * CF::N, cw);
-        }
-    }
-    __syncthreads();
-    block_copy_out<CF::N, KS<CF>::B>(a.nxt + b0 * CF::N, lds, nb);
-#ifdef M3_PHASE_PROF
-    if (live) st.end(0);
-#endif
-}
-
-// Finish the steps k_env_step paused (their cascade ran past KS::CASCADE_LIMIT
-// inner iterations): the long cascades of a launch, packed densely into waves
-// instead of holding every lane of their k_env_step wave idle. Grid-stride
-// over the records; each board is written straight to nxt.
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont(EnvArgs a) {
-    using K = KS<CF>;
-    // The few waves of this kernel are the step's critical path; they share SIMDs with
-    // the other shard's step waves and the resets: issue first (A/B: within noise).
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
-    const uint32_t cnt = a.counters[4];
-    LdsStore<CF, K::GCAP, K::B> st{tab + threadIdx.x};
-    st.spill = a.spill;
-    st.pool_next = &a.counters[3];
-    st.pool_cap = K::SPILL_RECORDS;
-    const int64_t cs = a.cont_stride;
-    for (uint32_t q = blockIdx.x * K::B + threadIdx.x; q < cnt; q += gridDim.x * K::B) {
-        const uint32_t* rec = a.cont + q;
-        const int64_t b = rec[0];
-        typename CF::Bd P[CF::NP];
-        typename K::Rng rng;
-        int r;
-        uint32_t f;
-        EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
-        const int mv = a.moves[b], sc0 = a.score[b];
-        typename CF::Bd HL, VL;
-        const bool dead = (f & FLAG_CONT_DEAD) != 0;  // settled with no legal move: continue at the shuffle
-        f &= ~FLAG_CONT_DEAD;
-        apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, -1, dead);
-        const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0);
-        if (!ok) {
-            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-            a.ovf_list[slot] = (uint32_t)b;
-        } else {
-            constexpr int NW = (CF::N + 3) / 4;
-            uint32_t cw[NW];
-            words_from_planes<CF>(P, cw);
-            store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.nxt + b * CF::N), cw);
-        }
-    }
-}
-
-template <class CF>
-__global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
-    const uint32_t cnt = a.counters[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], cnt);
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
-        const int64_t b = a.ovf_list[i];
-        typename CF::Bd P[CF::NP];
-        bytes_to_planes<CF>(a.cur + b * CF::N, P);
-        FullMT mt;  // scratch (see k_apply_fix)
-        mt.init(a.seeds[b], 0u);
-        ArrayStore<CF> st;
-        int r;
-        uint32_t f;
-        env_step_one<CF, false>(P, a, b, mt, st, -1, r, f);
-        planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * CF::N));
-    }
-}
-
-// ---------------------------------------------------------------------------
-// batched MCTS rollouts (mctslib/standard/mcts.py:14-19)
-// ---------------------------------------------------------------------------
-// One rollout per lane: np.random.seed(rseed); while n_actions >= 1:
-// action = choice(legal_actions) from the global stream, state =
-// apply_action(action). The first choice reads the stream of rseed; every
-// later one reads the stream apply_action left behind (cfg.seed reseeded at
-// boardv2.py:46, advanced by the step's draws), i.e. the same register chain
-// the step just used. The match-group table is the env's LDS table + spill
-// pool, and a lane keeps its spill record for the whole rollout; a rollout
-// that overflows the chain (>= 624 draws in one step) or the pool is
-// replayed from its first move by k_rollout_fix.
-struct RolloutArgs {
-    int64_t n;
-    const int8_t* boards;
-    const uint32_t* seeds;     // cfg.seed of each state
-    const int32_t* n_actions;
-    const uint32_t* rseeds;    // rollout seed (random.randint(0, 2**31 - 1) or state.seed)
-    int32_t* gain;             // sum of the step rewards of the rollout
-    int32_t* steps;            // apply_action calls
-    uint32_t* draws;           // global-stream draws since its last seed when the rollout ends
-    uint32_t* flags;           // OR of the steps' M3_FLAG_*
-    int8_t* out_boards;        // nullable: terminal boards
-    uint32_t* counters;        // [0] overflow count, [1] spill records taken
-    uint32_t* ovf_list;
-    uint32_t* spill;
-    uint32_t spill_cap;
-};
-
-template <class CF, class RNG, class Store>
-__device__ __forceinline__ bool rollout_one(typename CF::Bd* P, const RolloutArgs& a, int64_t b, RNG& first, RNG& rng,
-                                            Store& st) {
-    int n = a.n_actions[b];
-    int gain = 0, steps = 0;
-    uint32_t fl = 0u, dr = 0u;
-    if (n >= 1) {                                               // mcts.py:16 while not is_terminal
-        typename CF::Bd HL, VL;
-        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);
-        uint32_t act[CF::AW];
-        action_bits<CF>(HL, VL, act);
-        int x = random_action<CF>(act, first);                  // mcts.py:17, stream of the rollout seed
-        dr = first.draws();
-        for (;;) {
-            if (x < 0) {                                        // np.random.choice([]) raises
-                fl |= FLAG_NO_LEGAL;
-                break;
-            }
-            uint32_t f;
-            const int r = apply_action<CF>(P, n, x, rng, f, HL, VL, st);  // mcts.py:18
-            if (f & FLAG_RECOMPUTE) return false;
-            fl |= f;
-            gain += r;
-            ++steps;
-            --n;
-            dr = rng.draws();
-            if (n < 1) break;
-            action_bits<CF>(HL, VL, act);
-            x = random_action<CF>(act, rng);                    // stream where apply_action left it
-            if (rng.overflow) return false;
-            dr = rng.draws();
-        }
-    }
-    a.gain[b] = gain;
-    a.steps[b] = steps;
-    a.draws[b] = dr;
-    a.flags[b] = fl;
-    return true;
-}
-
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_rollout(RolloutArgs a) {
-    using K = KS<CF>;
-    static_assert(K::B == 64, "staging/table aliasing assumes one wave per workgroup");
-    // staging and match-group table share the LDS (as in k_env_step)
-    constexpr int STAGE_WORDS = (K::B * CF::N + 16 + 3) / 4;
-    constexpr int TAB_WORDS = LdsStore<CF, K::GCAP, K::B>::WORDS;
-    __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
-    uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
-    const int64_t b0 = (int64_t)blockIdx.x * K::B;
-    const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
-    block_copy_in<CF::N, K::B>(a.boards + b0 * CF::N, lds, nb);
-    __syncthreads();
-    const int t = threadIdx.x;
-    typename CF::Bd P[CF::NP];
-    if (t < nb) lds_to_planes<CF>(lds, t, P);
-    __syncthreads();
-    LdsStore<CF, K::GCAP, K::B> st{stage_tab + t};
-    st.spill = a.spill;
-    st.pool_next = &a.counters[1];
-    st.pool_cap = a.spill_cap;
-    if (t < nb) {
-        const int64_t b = b0 + t;
-        const uint32_t rs = a.rseeds[b], s = a.seeds[b];
-        typename K::Chain first, rng;  // a step past the chain's reach replays the rollout in k_rollout_fix
-        first.init(rs, mt_state397(rs));
-        rng.init(s, mt_state397(s));
-        if (!rollout_one<CF>(P, a, b, first, rng, st)) {
-            const uint32_t o = atomicAdd(&a.counters[0], 1u);
-            a.ovf_list[o] = (uint32_t)b;
-        }
-    }
-    if (!a.out_boards) return;
-    __syncthreads();
-    if (t < nb) planes_to_bytes<CF>(P, lds + t * CF::N);
-    __syncthreads();
-    block_copy_out<CF::N, K::B>(a.out_boards + b0 * CF::N, lds, nb);
-}
-
-// exact replay of overflowed rollouts: 624-word MT19937 states and the full
-// group table in lane-private scratch
-template <class CF>
-__global__ void __launch_bounds__(FIX_BLOCK) k_rollout_fix(RolloutArgs a) {
-    const uint32_t cnt = a.counters[0];
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
-        const int64_t b = a.ovf_list[i];
-        typename CF::Bd P[CF::NP];
-        bytes_to_planes<CF>(a.boards + b * CF::N, P);
-        FullMT first, rng;
-        first.init(a.rseeds[b], 0u);
-        rng.init(a.seeds[b], 0u);
-        ArrayStore<CF> st;
-        rollout_one<CF>(P, a, b, first, rng, st);
-        if (a.out_boards) {
-            uint8_t tmp[CF::N];
-            planes_to_bytes<CF>(P, tmp);
-            for (int x = 0; x < CF::N; ++x) a.out_boards[b * CF::N + x] = (int8_t)tmp[x];
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// shape dispatch
-// ---------------------------------------------------------------------------
-#define M3_SHAPES(X) \
-    X(9, 9, 6)       \
-    X(16, 16, 8)
-
-int shape_id(int r, int c, int t) {
-    int id = 0;
-#define X(R_, C_, T_)                                 \
-    if (r == R_ && c == C_ && t == T_) return id; \
-    ++id;
-    M3_SHAPES(X)
-#undef X
-    return -1;
-}
-
-}  // namespace
-
-// ---------------------------------------------------------------------------
-// host side
-// ---------------------------------------------------------------------------
-struct m3_ctx {
-    int device = 0;
-    int R = 0, C = 0, T = 0, N = 0, A = 0, AW = 0;
-    int shape = -1;
-    hipStream_t stream = nullptr;
-    // stateless scratch
-    void* dbuf = nullptr;
-    size_t dcap = 0;
-    uint32_t* counters = nullptr;  // [0] overflow count
-};
-
-struct m3_env {
-    m3_ctx* ctx = nullptr;
-    int64_t n = 0;
-    int num_moves = 20, goal = 500;
-    int autoreset = 0;
-    uint32_t stride = 0;
-    bool ready = false;
-    bool stale = false;  // fields were loaded with m3_env_set: rederive() before the next step
-    int8_t* boards[2] = {nullptr, nullptr};
-    int cur = 0;
-    uint32_t *seeds = nullptr, *flags = nullptr, *draws = nullptr, *legal = nullptr;
-    int32_t *score = nullptr, *moves = nullptr, *next_action = nullptr, *reward = nullptr;
-    uint8_t *done = nullptr, *trunc = nullptr;
-    // host-action steps (m3_env_step with actions): device copies and pinned
-    // staging, double-buffered by step parity like `packed`, uploaded on
-    // `ustream` (allocated on first use)
-    int32_t* actions[2] = {nullptr, nullptr};
-    int32_t* hstage[2] = {nullptr, nullptr};
-    hipStream_t ustream = nullptr;
-    hipEvent_t upload_ev[2] = {nullptr, nullptr};
-    bool upload_pend[2] = {false, false};  // upload_ev[p] recorded and not yet waited on by the host
-    bool upload_this = false;              // the step being enqueued reads actions[step & 1]
-    // counters, 64 words per shard: [8q + 0] step overflow count, [8q + 1]
-    // prefetch queue length, [8q + 2] prefetch overflow count, [8q + 3] spill
-    // records taken, [8q + 4] continuation records (q = step % PF_LAG); stats
-    // [40] step recomputes, [41] resets, [42] reset recomputes; [48 + k] the
-    // reset / slot-fill overflow counts (shard 0's block)
-    uint32_t* counters = nullptr;
-    uint32_t* ovf_list = nullptr;
-    uint32_t* spill = nullptr;  // group-table spill pools, one per shard slot
-    // NSLOT episode slots per board (see EnvArgs): the current episode's
-    // stream cache + the next episodes' initial state and cache
-    uint8_t* slot = nullptr;
-    uint32_t* ne_words = nullptr;
-    int32_t* ne_first = nullptr;
-    uint32_t* ne_legal = nullptr;
-    uint32_t* m397 = nullptr;  // [NSLOT][n]
-    uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont)
-    // prefetch queues and their overflow lists, by step % PF_LAG
-    uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {};
-    int64_t steps = 0;
-    int32_t* packed = nullptr;
-    int32_t* gathered = nullptr;
-    ncclComm_t comm = nullptr;
-    int nranks = 1, rank = 0;
-    // per-step kernel timing ring (bench.py roofline): event pair i brackets
-    // the i-th k_env_step launch since m3_env_timing(enable)
-    std::vector<hipEvent_t> tev;
-    int tcap = 0, tn = 0;
-    // Independent board shards, each with a step stream (step + fixup) and a
-    // prefetch stream (next-episode resets). Step t of a shard waits only for
-    // the prefetch of step t - PF_LAG, so resets overlap the following steps.
-    struct Shard {
-        int64_t off = 0, n = 0;
-        hipStream_t stream = nullptr, pstream = nullptr;
-        hipEvent_t ev = nullptr;       // last step work of this shard
-        hipEvent_t aev[2] = {};        // step work of the last step of each parity (reads actions[parity])
-        bool apending[2] = {};
-        hipEvent_t pev[PF_LAG] = {};   // prefetch of queue q done
-        bool ppending[PF_LAG] = {};
-        // counter block q already zeroed for its next step: by the reset, or on the
-        // prefetch stream after its last reader (ordered before that step by pev[q])
-        bool czero[PF_LAG] = {};
-    };
-    std::vector<Shard> shards;
-    // `packed` is double-buffered by step parity, so the RCCL gather of step t
-    // (context stream) overlaps step t+1; step t+2 waits for it (gev[buffer])
-    hipEvent_t gev[2] = {nullptr, nullptr};
-    bool gpend[2] = {false, false};
-};
+using namespace m3k;
 
 namespace {
+// rows < columns: the last action ids decode to a swap with the row below the
+// board, and the reference's legal_actions / apply_action raise IndexError on
+// every call (boardConfig.py:27,45-59; boardv2.py:188 calls legal_actions in
+// every step). Such a BoardConfig resets (BoardV2.__init__) but cannot step.
+int check_ids_on_board(const m3_ctx* c) {
+    if (c->R >= c->C) return M3_OK;
+    return set_err(M3_ERR_INVALID,
+                   "BoardConfig(rows=%d, columns=%d): action ids reach row %d, past the board; the reference's "
+                   "legal_actions / apply_action raise IndexError for rows < columns", c->R, c->C, c->R);
+}
 
 int ensure_scratch(m3_ctx* c, size_t bytes) {
     if (c->dcap >= bytes) return M3_OK;
@@ -1402,171 +69,12 @@ size_t carve_size(std::initializer_list<size_t> sizes) {
     return s + 256;
 }
 
-template <class CF>
-int grid_for(int64_t n) { return (int)((n + KS<CF>::B - 1) / KS<CF>::B); }
 
-template <class CF>
-int launch_apply(m3_ctx* c, const ApplyArgs& a) {
-    if (a.n == 0) return M3_OK;
-    HIP_TRY(hipMemsetAsync(a.ovf_count, 0, sizeof(uint32_t), c->stream));
-    hipLaunchKernelGGL(k_apply<CF>, dim3(grid_for<CF>(a.n)), dim3(KS<CF>::B), 0, c->stream, a);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_apply_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
-    HIP_TRY(hipGetLastError());
-    return M3_OK;
-}
 
-template <class CF>
-int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
-    if (max_items == 0) return M3_OK;
-    int64_t g = (max_items + INIT_BLOCK - 1) / INIT_BLOCK;
-    if (g > 4096) g = 4096;
-    if constexpr (INIT_INLINE_FIX<CF>)
-        hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
-    else  // ~60% of 16x16x8 resets overflow the first MT block: FullMT for all
-        hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3((unsigned)g), dim3(INIT_FIX_BLOCK), 0, stream, a);
-    HIP_TRY(hipGetLastError());
-    return M3_OK;
-}
 
-template <class CF>
-int launch_legal(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* legal) {
-    if (n == 0) return M3_OK;
-    hipLaunchKernelGGL(k_legal<CF>, dim3(grid_for<CF>(n)), dim3(KS<CF>::B), 0, c->stream, n, boards, legal);
-    HIP_TRY(hipGetLastError());
-    return M3_OK;
-}
 
-// InitArgs of the prefetch (next-episode slots) of the boards from offset o.
-template <class CF>
-void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
-    r.sstride = e->n;
-    r.board_words = e->ne_words + o * ((CF::N + 3) / 4);
-    r.first_action = e->ne_first + o;
-    r.legal = e->ne_legal + o * CF::AW;
-    r.m397 = e->m397 + o;
-    r.cstride = e->n;
-}
 
-// Enqueue one env step of shard s: on the step stream, wait for the prefetch
-// of step t - PF_LAG (the queue and slots this step reuses), for the RCCL
-// gather of step t - 2 (same `packed` buffer) and, for host actions, for
-// their upload; zero this parity's counters, k_env_step (cur -> nxt, with
-// the in-step autoreset swap) and k_env_fix (exact recompute of overflowed
-// boards); on the prefetch stream, k_init + k_init_fix over the queued slots.
-// Every pointer is offset to the shard, so kernels see shard-local indices.
-template <class CF>
-int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
-    m3_ctx* c = e->ctx;
-    m3_env::Shard& sh = e->shards[s];
-    if (sh.n == 0) return M3_OK;
-    const int64_t o = sh.off;
-    const int N = c->N, AW = c->AW;
-    const int par = (int)(e->steps % PF_LAG);
-    uint32_t* base = e->counters + 64 * s;
-    uint32_t* cnt = base + 8 * par;
-    hipStream_t st = sh.stream;
-    const int pb = (int)(e->steps & 1);  // packed buffer of this step
-    if (e->upload_this) HIP_TRY(hipStreamWaitEvent(st, e->upload_ev[pb], 0));  // host actions in actions[pb]
-#ifndef M3_TEST_NO_GATHER_WAIT  // negative-control build for tests/test_gpu_dist.py only
-    if (e->gpend[pb]) HIP_TRY(hipStreamWaitEvent(st, e->gev[pb], 0));          // gather of step t-2 still reading
-#endif
-    if (sh.ppending[par]) HIP_TRY(hipStreamWaitEvent(st, sh.pev[par], 0));  // queue + slots of step t - PF_LAG
-    EnvArgs a;
-    a.n = sh.n;
-    a.num_moves = e->num_moves;
-    a.goal = e->goal;
-    a.autoreset = e->autoreset;
-    a.stride = e->stride;
-    a.cur = e->boards[e->cur] + o * N;
-    a.nxt = e->boards[e->cur ^ 1] + o * N;
-    a.actions = d_actions ? d_actions + o : nullptr;
-    a.seeds = e->seeds + o;
-    a.score = e->score + o;
-    a.moves = e->moves + o;
-    a.next_action = e->next_action + o;
-    a.reward = e->reward + o;
-    a.done = e->done + o;
-    a.trunc = e->trunc + o;
-    a.flags = e->flags + o;
-    a.draws = e->draws + o;
-    a.legal = e->legal + o * AW;
-    a.packed = e->comm ? e->packed + (size_t)pb * e->n + o : nullptr;  // only the RCCL gather reads it
-    a.counters = cnt;
-    a.spill = e->spill + (size_t)s * KS<CF>::SPILL_RECORDS * LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::SPILL_WORDS;
-    a.stats = base + 40;
-    a.ovf_list = e->ovf_list + o;
-    a.slot = e->slot + o;
-    a.ne_words = e->ne_words + o * ((N + 3) / 4);
-    a.ne_first = e->ne_first + o;
-    a.ne_legal = e->ne_legal + o * AW;
-    a.pf_list = e->pf_list[par] + o;
-    a.pf_seed = e->pf_seed[par] + o;
-    a.pf_slot = e->pf_slot[par] + o;
-    a.m397 = e->m397 + o;
-    a.cstride = e->n;
-    a.cont = KS<CF>::CASCADE_LIMIT >= 0 ? e->cont + o : nullptr;
-    a.cont_stride = e->n;
-    if (!sh.czero[par]) HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), st));
-    sh.czero[par] = false;
-    const bool timed = e->tn < e->tcap;
-    if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], st));
-    // launches that grid-stride over a device-side count are sized for its usual share of the shard
-    auto frac_grid = [&](double f) {
-        const int64_t g = ((int64_t)(sh.n * f) + KS<CF>::B - 1) / KS<CF>::B;
-        return dim3((unsigned)(g > 0 ? g : 1));
-    };
-    hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
-    HIP_TRY(hipGetLastError());
-    if (a.cont) {  // sized for the share of paused steps (~20 % at limit 2)
-        hipLaunchKernelGGL(k_env_cont<CF>, frac_grid(0.25), dim3(KS<CF>::B), 0, st, a);
-        HIP_TRY(hipGetLastError());
-    }
-    hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
-    HIP_TRY(hipGetLastError());
-    if (timed) {  // the whole step pipeline of the shard, fixup pass included
-        HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], st));
-        e->tn++;
-    }
-    HIP_TRY(hipEventRecord(sh.ev, st));
-    if (e->upload_this) {  // the upload two steps ahead rewrites actions[pb] once this shard has read it
-        HIP_TRY(hipEventRecord(sh.aev[pb], st));
-        sh.apending[pb] = true;
-    }
-    if (e->autoreset) {
-        HIP_TRY(hipStreamWaitEvent(sh.pstream, sh.ev, 0));
-        InitArgs r{};
-        r.n = sh.n;
-        r.list = e->pf_list[par] + o;
-        r.list_seed = e->pf_seed[par] + o;
-        r.list_slot = e->pf_slot[par] + o;
-        r.list_count = &cnt[1];
-        r.stats = base + 41;
-        prefetch_args<CF>(e, o, r);
-        // the grid is sized for the expected number of finished boards and grid-strides
-        int rc = launch_init<CF>(sh.pstream, r, sh.n / 8 + 1);
-        if (rc) return rc;
-        // the resets were the block's last readers: zero it here, off the step's critical path
-        HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), sh.pstream));
-        HIP_TRY(hipEventRecord(sh.pev[par], sh.pstream));
-        sh.ppending[par] = true;
-        sh.czero[par] = true;
-    }
-    return M3_OK;
-}
 
-template <class CF>
-int launch_env_step(m3_env* e, const int32_t* d_actions) {
-    for (int s = 0; s < (int)e->shards.size(); ++s) {
-        int rc = launch_env_shard<CF>(e, s, d_actions);
-        if (rc) return rc;
-    }
-    e->upload_this = false;
-    e->gpend[e->steps & 1] = false;
-    e->cur ^= 1;
-    e->steps++;
-    return M3_OK;
-}
 
 // Make `st` wait for every shard's last enqueued work.
 int join_shards(m3_env* e, hipStream_t st) {
@@ -1598,68 +106,23 @@ void destroy_shards(m3_env* e) {
     }
     e->shards.clear();
 }
-
-// Episode slots cur + 1 .. cur + NSLOT - 1 of every board from its current
-// seed (explicit reset, or autoreset switched on later).
-template <class CF>
-int fill_next_slots(m3_env* e) {
-    m3_ctx* c = e->ctx;
-    for (uint32_t k = 1; k < (uint32_t)NSLOT; ++k) {
-        InitArgs r{};
-        r.n = e->n;
-        r.seeds = e->seeds;
-        r.seed_add = k * e->stride;
-        r.slot0 = k;
-        r.slot_of = e->slot;
-        prefetch_args<CF>(e, 0, r);
-        int rc = launch_init<CF>(c->stream, r, e->n);
-        if (rc) return rc;
-    }
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return M3_OK;
-}
-
-// After m3_env_set: rebuild what the env derives from the loaded fields --
-// every board back in episode slot 0, the chain word mt[397] of its seed, the
-// legal set of its board, the queued next episodes -- and restart the step
-// counter, exactly the state m3_env_reset leaves behind for those fields.
-template <class CF>
-int rederive(m3_env* e) {
-    m3_ctx* c = e->ctx;
-    HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));
-    HIP_TRY(hipMemsetAsync(e->slot, 0, e->n, c->stream));
-    const int64_t g = std::min<int64_t>((e->n + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_mt397, dim3((unsigned)g), dim3(256), 0, c->stream, e->n, e->seeds, e->m397);
-    HIP_TRY(hipGetLastError());
-    int rc = launch_legal<CF>(c, e->n, e->boards[e->cur], e->legal);
-    if (rc) return rc;
-    e->steps = 0;
-    e->gpend[0] = e->gpend[1] = false;
-    for (auto& sh : e->shards)
-        for (bool& z : sh.czero) z = true;  // (the memset above; this ends with a sync)
-    if (e->autoreset) {
-        rc = fill_next_slots<CF>(e);
-        if (rc) return rc;
-    }
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    e->stale = false;
-    return M3_OK;
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+// configuration id (shape_id) -> its config type (CF_<id>, m3_kernels.hpp)
 template <class F>
 static int with_shape(int shape, F&& f) {
-    int id = 0;
-#define X(R_, C_, T_)                                 \
-    if (shape == id) return f(Cfg<R_, C_, T_>{}); \
-    ++id;
-    M3_SHAPES(X)
-#undef X
-    return set_err(M3_ERR_UNSUPPORTED, "board shape not compiled in");
+    static_assert(N_CONFIGS == 5, "with_shape lists every configuration");
+    switch (shape) {
+        case 0: return f(CF_0{});
+        case 1: return f(CF_1{});
+        case 2: return f(CF_2{});
+        case 3: return f(CF_3{});
+        case 4: return f(CF_4{});
+        default: return set_err(M3_ERR_UNSUPPORTED, "board shape not compiled in");
+    }
 }
 
 static int ensure_fresh(m3_env* e) {
@@ -1696,8 +159,9 @@ int m3_ctx_create(int device, int rows, int columns, int types, m3_ctx** out) {
     *out = nullptr;
     const int sid = shape_id(rows, columns, types);
     if (sid < 0)
-        return set_err(M3_ERR_UNSUPPORTED, "BoardConfig(rows=%d, columns=%d, types=%d) is not compiled in", rows,
-                       columns, types);
+        return set_err(M3_ERR_UNSUPPORTED,
+                       "BoardConfig(rows=%d, columns=%d, types=%d): supported are rows and columns 3..16, "
+                       "types 3..15", rows, columns, types);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return set_err(M3_ERR_NO_DEVICE, "no HIP device visible (libm3 has no CPU fallback)");
@@ -1716,6 +180,7 @@ int m3_ctx_create(int device, int rows, int columns, int types, m3_ctx** out) {
     c->A = rows * (columns - 1) * 2;
     c->AW = (c->A + 31) / 32;
     c->shape = sid;
+    c->sdesc = make_shape(rows, columns, types);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->counters, 256);
     if (e != hipSuccess) {
@@ -1760,6 +225,7 @@ int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boar
     HIP_TRY(hipMemcpyAsync(d_seeds, seeds, n * 4, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->counters, 0, 16, c->stream));
     InitArgs a{};
+    a.shape = c->sdesc;
     a.n = n;
     a.seeds = d_seeds;
     a.boards = d_boards;
@@ -1781,6 +247,8 @@ int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t*
     if (n == 0) return M3_OK;
     CHECK_ARG(boards && seeds && n_actions && actions && out_boards && out_reward && out_draws && out_flags,
               "null buffer");
+    int rc0 = check_ids_on_board(c);
+    if (rc0) return rc0;
     for (int64_t i = 0; i < n * c->N; ++i)
         if (boards[i] < 0) return set_err(M3_ERR_INVALID, "cell value outside [0, 127] at byte %lld", (long long)i);
     HIP_TRY(hipSetDevice(c->device));
@@ -1791,6 +259,7 @@ int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t*
     if (rc) return rc;
     Carve cv{(char*)c->dbuf};
     ApplyArgs a{};
+    a.shape = c->sdesc;
     a.n = n;
     int8_t* d_in = cv.take<int8_t>(bytes);
     uint32_t* d_seeds = cv.take<uint32_t>(n);
@@ -1830,6 +299,8 @@ int m3_legal_actions(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* out_l
     CHECK_ARG(c && n >= 0, "bad arguments");
     if (n == 0) return M3_OK;
     CHECK_ARG(boards && out_legal_bits, "null buffer");
+    int rc0 = check_ids_on_board(c);
+    if (rc0) return rc0;
     HIP_TRY(hipSetDevice(c->device));
     const size_t bytes = n * (size_t)c->N;
     int rc = ensure_scratch(c, carve_size({bytes, n * 4ull * c->AW}));
@@ -1869,14 +340,7 @@ int enqueue_rollouts(m3_ctx* c, RolloutArgs a, Carve& cv) {
     a.spill = cv.take<uint32_t>(cap * rollout_spill_words(c->shape));
     a.spill_cap = (uint32_t)cap;
     HIP_TRY(hipMemsetAsync(c->counters, 0, 16, c->stream));
-    return with_shape(c->shape, [&](auto cf) {
-        using CF = decltype(cf);
-        hipLaunchKernelGGL(k_rollout<CF>, dim3(grid_for<CF>(a.n)), dim3(KS<CF>::B), 0, c->stream, a);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_rollout_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
-        HIP_TRY(hipGetLastError());
-        return M3_OK;
-    });
+    return with_shape(c->shape, [&](auto cf) { return launch_rollouts<decltype(cf)>(c, a); });
 }
 
 }  // namespace
@@ -1891,11 +355,14 @@ int m3_rollouts_device(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_
     CHECK_ARG(n < (int64_t)1 << 31, "n too large");
     CHECK_ARG(boards && seeds && n_actions && rollout_seeds && out_gain && out_steps && out_draws && out_flags,
               "null buffer");
+    int rc0 = check_ids_on_board(c);
+    if (rc0) return rc0;
     HIP_TRY(hipSetDevice(c->device));
     int rc = ensure_scratch(c, carve_size({n * 4ull, rollout_spill_cap(n) * rollout_spill_words(c->shape) * 4ull}));
     if (rc) return rc;
     Carve cv{(char*)c->dbuf};
     RolloutArgs a{};
+    a.shape = c->sdesc;
     a.n = n;
     a.boards = boards;
     a.seeds = seeds;
@@ -1917,6 +384,8 @@ int m3_rollouts(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seed
     CHECK_ARG(n < (int64_t)1 << 31, "n too large");
     CHECK_ARG(boards && seeds && n_actions && rollout_seeds && out_gain && out_steps && out_draws && out_flags,
               "null buffer");
+    int rc0 = check_ids_on_board(c);
+    if (rc0) return rc0;
     for (int64_t i = 0; i < n * c->N; ++i)
         if (boards[i] < 0) return set_err(M3_ERR_INVALID, "cell value outside [0, 127] at byte %lld", (long long)i);
     HIP_TRY(hipSetDevice(c->device));
@@ -1928,6 +397,7 @@ int m3_rollouts(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seed
     if (rc) return rc;
     Carve cv{(char*)c->dbuf};
     RolloutArgs a{};
+    a.shape = c->sdesc;
     a.n = n;
     int8_t* d_in = cv.take<int8_t>(bytes);
     uint32_t* d_seeds = cv.take<uint32_t>(n);
@@ -1961,6 +431,8 @@ int m3_rollouts(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seed
 int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** out) {
     CHECK_ARG(c && out && n > 0 && num_moves > 0, "bad arguments");
     CHECK_ARG(n < (int64_t)1 << 31, "n too large");
+    int rc0 = check_ids_on_board(c);
+    if (rc0) return rc0;
     *out = nullptr;
     HIP_TRY(hipSetDevice(c->device));
     m3_env* e = new m3_env;
@@ -2103,6 +575,7 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
         HIP_TRY(err);
     }
     InitArgs a{};
+    a.shape = c->sdesc;
     a.n = e->n;
     a.seeds = e->seeds;
     a.boards = e->boards[e->cur];
@@ -2378,16 +851,27 @@ int m3_env_stats(m3_env* e, uint64_t out[4]) {
 }
 
 #ifdef M3_PHASE_PROF
-// profiling build only (not part of include/m3.h): out[2][PH_N + 2]
+// profiling build only (not part of include/m3.h): out[2][PH_N + 2], summed over the
+// configurations' translation units (each has its own g_prof)
+#ifdef M3_SPLIT_TU
+extern "C" int m3_prof_read_0(uint64_t*, int), m3_prof_read_1(uint64_t*, int), m3_prof_read_2(uint64_t*, int),
+    m3_prof_read_3(uint64_t*, int), m3_prof_read_4(uint64_t*, int);
 int m3_prof_read(uint64_t* out, int reset) {
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)));
-    if (reset) {
-        static const unsigned long long zero[2][PROF_SLOTS] = {};
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), zero, sizeof(zero)));
+    static_assert(N_CONFIGS == 5, "one reader per configuration");
+    int (*const rd[5])(uint64_t*, int) = {m3_prof_read_0, m3_prof_read_1, m3_prof_read_2, m3_prof_read_3,
+                                         m3_prof_read_4};
+    uint64_t part[2 * PROF_SLOTS];
+    for (int i = 0; i < 2 * PROF_SLOTS; ++i) out[i] = 0;
+    for (auto f : rd) {
+        const int rc = f(part, reset);
+        if (rc < 0) return rc;
+        for (int i = 0; i < 2 * PROF_SLOTS; ++i) out[i] += part[i];
     }
     return PH_N;
 }
+#else
+int m3_prof_read(uint64_t* out, int reset) { return m3_prof_read_tu(out, reset); }
+#endif
 #endif
 
 int m3_env_timing(m3_env* e, int capacity) {

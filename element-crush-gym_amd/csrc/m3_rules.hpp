@@ -54,11 +54,24 @@ enum : uint32_t {
     FLAG_RNG_OVERFLOW = 0x20u, // internal: step needed >= 624 draws; recomputed with FullMT
     FLAG_GROUP_OVERFLOW = 0x40u, // internal: more match groups than the fast table holds; recomputed
     FLAG_RECOMPUTE = FLAG_RNG_OVERFLOW | FLAG_GROUP_OVERFLOW,
+    FLAG_CASCADE_CAP = 0x100u, // cascade stopped after CASCADE_CAP refills (reference: unbounded)
 };
+// Refill-and-rematch passes one step may run. The reference loops until a
+// refill leaves no match (boardv2.py:138-202); with few tile types on a large
+// board (types = 2) that practically never happens, and a GPU lane must end.
+// Steps of the supported shapes use 1-10 passes; the cap is a
+// safety bound, flagged when hit (parity undefined there, as at the shuffle cap).
+constexpr int CASCADE_CAP = 1024;
+
+template <class CF>
+struct StaticDim;
+template <class CF>
+struct FrameDim;
 
 // BoardConfig (match3tile/boardConfig.py:26-43) as compile-time constants.
 template <int R_, int C_, int T_>
 struct Cfg {
+    static constexpr bool DYN = false;  // shape fixed at compile time (see FCfg)
     static constexpr int R = R_, C = C_, T = T_;
     static constexpr int N = R * C;
     static constexpr int W = (N + 31) / 32;
@@ -78,9 +91,144 @@ struct Cfg {
     static constexpr uint32_t TILE_RNG = (uint32_t)(T - 1);
     static constexpr uint32_t TILE_MASK = (1u << ceil_log2(T)) - 1u;
     static_assert(R >= 4 && C >= 4 && R <= 16 && C <= 16, "board size");
-    static_assert(T >= 1 && BITS <= 4, "tile types must fit 4 bits");
+    static_assert(T >= 2 && BITS <= 4, "tile types must fit 4 bits");
     using Bd = BB<W>;
     using G = Geo<R, C, W>;
+    using Dim = StaticDim<Cfg>;
+};
+
+// Any other BoardConfig(rows, columns, types) with 3 <= rows, columns <= 16
+// and 2 <= types <= 15 runs in a 16 x 16 FRAME: cell (r, c) is bit r*16 + c,
+// so the row stride -- every shift the rule code uses -- is a compile-time 16
+// for every board width, and only BITS (the token layout, boardConfig.py:29-33)
+// is a template parameter. The board's own rows / columns / types / action
+// count are run-time values (FrameDim). Cells outside the board ("walls")
+// hold 0 in every plane: they never start or extend a run (get_matches skips
+// 0, boardFunctions.py:136), never equal a non-zero token in the legal-move
+// patterns (so the reference's bounds checks, boardFunctions.py:42-92, hold
+// by construction), and are kept out of every cleared / empty / refilled set
+// by the board mask. (Rows < columns are accepted for reset only: the
+// reference's action ids then reach past the last row and legal_actions /
+// apply_action raise IndexError, boardConfig.py:27,45-59.)
+template <int BITS_>
+struct FCfg {
+    static constexpr bool DYN = true;
+    static constexpr int R = 16, C = 16;  // the frame (row stride 16)
+    static constexpr int N = R * C;
+    static constexpr int W = N / 32;
+    static constexpr int BITS = BITS_;
+    static constexpr int TM = (1 << BITS) - 1;
+    static constexpr int STM = (1 << (BITS + 1)) + 1 + TM;
+    static constexpr int H = TM + 1;
+    static constexpr int V = 2 * H;
+    static constexpr int B = STM;
+    static constexpr int M = TM + STM + 1;
+    static constexpr int A = R * (C - 1) * 2;    // upper bounds: the board's are FrameDim's
+    static constexpr int AW = (A + 31) / 32;
+    static constexpr int NP = 7;
+    static constexpr int MAXG = N / 3 + 1;
+    static constexpr int SHUFFLE_CAP = 1024;
+    static_assert(BITS >= 2 && BITS <= 4, "types 2..15");
+    using Bd = BB<W>;
+    using G = Geo<R, C, W>;
+    using Dim = FrameDim<FCfg>;
+};
+
+constexpr int bits_for_types(int t) { return ceil_log2(t + 1); }
+
+// A board shape at run time (kernel argument of the frame kernels): the
+// BoardConfig fields plus, per frame cell x, whether the swap (x, x+1) /
+// (x, x+16) is the decode of some action id < A. Those are the only swaps
+// legal_actions can return (boardFunctions.py:97 iterates cfg.actions), and
+// on most non-square boards they are not all of them: with C = 3 the literal
+// 3 of boardConfig.py:50 sends the vertical ids of row r to row r-1, and when
+// rows > columns the id range A = R(C-1)*2 (boardConfig.py:27) ends inside a
+// row. The dead-board test (boardv2.py:188) is "no legal id", so it must see
+// exactly these swaps.
+struct Shape {
+    int rows, cols, types;
+    uint32_t hreach[8], vreach[8];
+};
+
+// decode (boardConfig.py:45-59) -> the first cell of the swap, and whether it is vertical
+M3_HD void decode_action(int action, int cols, int& r, int& c, bool& vertical) {
+    const int AR = 2 * cols - 1, BR = cols - 1;
+    if (action % AR >= BR) {
+        c = action % AR - BR;
+        r = (action - 3 - c) / AR;  // C / C++ division truncates toward 0, as Python's int()
+        vertical = true;
+    } else {
+        c = action % AR;
+        r = (action - c) / AR;
+        vertical = false;
+    }
+}
+
+M3_HD Shape make_shape(int rows, int cols, int types) {
+    Shape s;
+    s.rows = rows;
+    s.cols = cols;
+    s.types = types;
+    for (int i = 0; i < 8; ++i) s.hreach[i] = s.vreach[i] = 0u;
+    const int A = rows * (cols - 1) * 2;
+    for (int a = 0; a < A; ++a) {
+        int r, c;
+        bool v;
+        decode_action(a, cols, r, c, v);
+        const int x = r * 16 + c;
+        if (x < 0 || x >= 256) continue;
+        (v ? s.vreach : s.hreach)[x >> 5] |= 1u << (x & 31);
+    }
+    return s;
+}
+
+// The board shape as the rule code reads it. For a Cfg every accessor is a
+// compile-time constant (the specialised kernels compile exactly as if the
+// constants were written in place); for an FCfg they are the run-time values
+// of the board in its frame.
+template <class CF>
+struct StaticDim {
+    M3_HD constexpr StaticDim() {}
+    M3_HD constexpr StaticDim(const Shape&) {}
+    M3_HD static constexpr int rows() { return CF::R; }
+    M3_HD static constexpr int cols() { return CF::C; }
+    M3_HD static constexpr int cells() { return CF::N; }
+    M3_HD static constexpr int actions() { return CF::A; }
+    M3_HD static constexpr int aw() { return CF::AW; }
+    M3_HD static constexpr uint32_t tile_rng() { return CF::TILE_RNG; }
+    M3_HD static constexpr uint32_t tile_mask() { return CF::TILE_MASK; }
+    M3_HD static constexpr typename CF::Bd valid() { return CF::G::valid(); }
+};
+
+template <class CF>
+struct FrameDim {
+    using Bd = typename CF::Bd;
+    int r, c, a;
+    uint32_t trng, tmask;
+    Bd vmask;      // board cells
+    Bd hl, vl;     // swaps (x, x+1) / (x, x+16) that some action id decodes to (Shape)
+    M3_HD FrameDim(const Shape& s) : r(s.rows), c(s.cols), a(s.rows * (s.cols - 1) * 2) {
+        trng = (uint32_t)(s.types - 1);                      // randint(1, T+1)
+        uint32_t m = trng;
+        m |= m >> 1; m |= m >> 2; m |= m >> 4;
+        tmask = m;
+        const uint32_t row = (1u << c) - 1u;
+#pragma unroll
+        for (int i = 0; i < CF::W; ++i) {
+            const int r0 = 2 * i, r1 = 2 * i + 1;
+            vmask.w[i] = (r0 < r ? row : 0u) | (r1 < r ? row << 16 : 0u);
+            hl.w[i] = s.hreach[i];
+            vl.w[i] = s.vreach[i];
+        }
+    }
+    M3_HD int rows() const { return r; }
+    M3_HD int cols() const { return c; }
+    M3_HD int cells() const { return r * c; }
+    M3_HD int actions() const { return a; }
+    M3_HD int aw() const { return (a + 31) / 32; }
+    M3_HD uint32_t tile_rng() const { return trng; }
+    M3_HD uint32_t tile_mask() const { return tmask; }
+    M3_HD Bd valid() const { return vmask; }
 };
 
 // boards of at least this many words take the word-sliced legal_masks (0: never)
@@ -234,8 +382,8 @@ M3_HD void legal_words(const typename CF::Bd* P, const typename CF::Bd& z0, cons
 }
 
 template <class CF>
-M3_HD void legal_masks(const typename CF::Bd* P, const typename CF::Bd& spec,
-                       typename CF::Bd& HL, typename CF::Bd& VL) {
+M3_HD void legal_masks_all(const typename CF::Bd* P, const typename CF::Bd& spec,
+                           typename CF::Bd& HL, typename CF::Bd& VL) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
     constexpr int C = CF::C, R = CF::R;
@@ -285,6 +433,18 @@ M3_HD void legal_masks(const typename CF::Bd* P, const typename CF::Bd& spec,
     }
 }
 
+// In a frame (FCfg) the patterns above run over the whole 16 x 16 frame; only
+// swaps with both cells on the board are actions.
+template <class CF>
+M3_HD void legal_masks(const typename CF::Bd* P, const typename CF::Bd& spec, typename CF::Bd& HL,
+                       typename CF::Bd& VL, const typename CF::Dim& dm = typename CF::Dim{}) {
+    legal_masks_all<CF>(P, spec, HL, VL);
+    if constexpr (CF::DYN) {
+        HL &= dm.hl;
+        VL &= dm.vl;
+    }
+}
+
 // legal bits in action-id order (BoardConfig.actions, boardConfig.py:37,45-59):
 // row r owns ids r*(2C-1) .. ; first C-1 horizontal (r,c)-(r,c+1), then C vertical.
 template <class CF, int ROW = 0>
@@ -301,11 +461,48 @@ M3_HD void action_bits_rows(const typename CF::Bd& HL, const typename CF::Bd& VL
         action_bits_rows<CF, ROW + 1>(HL, VL, act);
     }
 }
+// Frame form: the board's row length L = 2C-1 is a run-time value, so output
+// word i collects, for every id-row r, the bits of its field f_r that land in
+// [32i, 32i+32) (compile-time indices only: no dynamic register indexing).
+// Vertical ids of id-row r decode to cell row int((r*L + C-1 - 3) / L)
+// (boardConfig.py:50's literal 3): r for C >= 4, r - 1 (0 for r = 0) for C = 3.
+// Ids >= A (the last row's missing swaps, boardConfig.py:27) are dropped.
 template <class CF>
-M3_HD void action_bits(const typename CF::Bd& HL, const typename CF::Bd& VL, uint32_t* act) {
+M3_HD void action_bits_frame(const typename CF::Bd& HL, const typename CF::Bd& VL, uint32_t* act,
+                             const typename CF::Dim& dm) {
+    const int C = dm.cols(), L = 2 * C - 1, A = dm.actions();
+    const uint32_t hm = (1u << (C - 1)) - 1u, vm = (1u << C) - 1u;
+    uint32_t f[CF::R];
 #pragma unroll
-    for (int i = 0; i < CF::AW; ++i) act[i] = 0u;
-    action_bits_rows<CF, 0>(HL, VL, act);
+    for (int r = 0; r < CF::R; ++r) {
+        const uint32_t h = (HL.w[r >> 1] >> ((r & 1) * 16)) & hm;
+        const int rp = r > 0 ? r - 1 : 0;
+        const uint32_t v = C == 3 ? (VL.w[rp >> 1] >> ((rp & 1) * 16)) & vm : (VL.w[r >> 1] >> ((r & 1) * 16)) & vm;
+        f[r] = r < dm.rows() ? (h | (v << (C - 1))) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < CF::AW; ++i) {
+        uint32_t w = 0u;
+#pragma unroll
+        for (int r = 0; r < CF::R; ++r) {
+            const int sh = r * L - 32 * i;
+            if (sh > -L && sh < 32) w |= sh >= 0 ? (f[r] << sh) : (f[r] >> -sh);
+        }
+        const int lim = A - 32 * i;
+        act[i] = lim >= 32 ? w : (lim <= 0 ? 0u : (w & ((1u << lim) - 1u)));
+    }
+}
+
+template <class CF>
+M3_HD void action_bits(const typename CF::Bd& HL, const typename CF::Bd& VL, uint32_t* act,
+                       const typename CF::Dim& dm = typename CF::Dim{}) {
+    if constexpr (CF::DYN) {
+        action_bits_frame<CF>(HL, VL, act, dm);
+    } else {
+#pragma unroll
+        for (int i = 0; i < CF::AW; ++i) act[i] = 0u;
+        action_bits_rows<CF, 0>(HL, VL, act);
+    }
 }
 
 
@@ -535,10 +732,12 @@ M3_HD void py_slice(int start, int stop, int n, int& lo, int& hi) {
 // special tokens whose TB is zero fire (:141-154); SP is not refreshed inside
 // the pass, so the effects are a union and order does not matter.
 template <class CF, int NPU>
-M3_HD typename CF::Bd fire_specials(const typename CF::Bd* P, typename CF::Bd z) {
+M3_HD typename CF::Bd fire_specials(const typename CF::Bd* P, typename CF::Bd z,
+                                   const typename CF::Dim& dm = typename CF::Dim{}) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
-    constexpr int BITS = CF::BITS, C = CF::C, R = CF::R;
+    constexpr int BITS = CF::BITS, C = CF::C;
+    const int R = dm.rows(), CB = dm.cols();  // slice lengths: the board's
     const Bd spz = z & special_mask<CF, NPU>(P);
     const Bd kh = P[BITS].andnot(P[BITS + 1]);   // (x & STM) == H
     const Bd kv = P[BITS + 1].andnot(P[BITS]);   // (x & STM) == V
@@ -556,10 +755,11 @@ M3_HD typename CF::Bd fire_specials(const typename CF::Bd* P, typename CF::Bd z)
         } else {                                            // token_board[j-1:j+1, i-1:i+1] = 0
             int rl, rh, cl, ch;
             py_slice(j - 1, j + 1, R, rl, rh);
-            py_slice(i - 1, i + 1, C, cl, ch);
+            py_slice(i - 1, i + 1, CB, cl, ch);
             add |= G::row_band(rl, rh) & G::col_band(cl, ch);
         }
     }
+    if constexpr (CF::DYN) return (z | add) & dm.valid();  // frame rows / columns reach into the walls
     return z | add;
 }
 
@@ -612,11 +812,10 @@ M3_HD void merge_clip(typename CF::Bd* P, const typename CF::Bd& z, const typena
 // order (new[0] at row 0). Tiles come from randint(1, T+1).
 // gravity: returns the (top-aligned) empty cells
 template <class CF>
-M3_HD typename CF::Bd gravity(typename CF::Bd* P) {
+M3_HD typename CF::Bd gravity(typename CF::Bd* P, const typename CF::Dim& dm = typename CF::Dim{}) {
     using Bd = typename CF::Bd;
-    using G = typename CF::G;
     constexpr int C = CF::C, R = CF::R, NPU = 6;
-    constexpr Bd VALID = G::valid();
+    const Bd VALID = dm.valid();  // walls are neither holes nor tiles
     Bd occ = P[0];
 #pragma unroll
     for (int p = 1; p < NPU; ++p) occ |= P[p];
@@ -641,7 +840,8 @@ M3_HD typename CF::Bd gravity(typename CF::Bd* P) {
 
 // refill of the top-aligned empty cells em
 template <class CF, class RNG>
-M3_HD void refill(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng) {
+M3_HD void refill(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng,
+                  const typename CF::Dim& dm = typename CF::Dim{}) {
     using Bd = typename CF::Bd;
     constexpr int C = CF::C, R = CF::R;
     if (!em.any()) return;
@@ -651,16 +851,12 @@ M3_HD void refill(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng) {
     // One raw draw per loop trip (the masked-rejection of randint(1, T+1) is
     // folded into the trip count): with a nested rejection loop per tile the
     // wave would wait for its unluckiest lane on every tile.
+    const uint32_t tmask = dm.tile_mask(), trng = dm.tile_rng();
     for (;;) {
-        uint32_t v;
-        if constexpr (CF::TILE_RNG == 0u) {
-            v = 1u;
-        } else {
-            v = rng.next32() & CF::TILE_MASK;
-            if (rng.overflow) break;
-            if (v > CF::TILE_RNG) continue;
-            v += 1u;                                       // randint(1, T+1)
-        }
+        uint32_t v = rng.next32() & tmask;
+        if (rng.overflow) break;
+        if (v > trng) continue;
+        v += 1u;                                           // randint(1, T+1)
         const int x = r * C + c;
         const Bd bm = Bd::bit_at(x);
 #pragma unroll
@@ -683,7 +879,7 @@ M3_HD void refill(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng) {
 // shuffle (boardFunctions.py:16-23): reseed, Fisher-Yates over rows with
 // random_interval, then put every special back at its original cell.
 template <class CF, class RNG>
-M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng) {
+M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng, const typename CF::Dim& dm = typename CF::Dim{}) {
     using Bd = typename CF::Bd;
     constexpr int C = CF::C, R = CF::R, NPU = 6;
     rng.reseed();
@@ -691,7 +887,7 @@ M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng) {
     uint64_t idx = 0;  // nibble i = source row of row i
 #pragma unroll
     for (int i = 0; i < R; ++i) idx |= (uint64_t)i << (4 * i);
-    for (int i = R - 1; i >= 1; --i) {
+    for (int i = dm.rows() - 1; i >= 1; --i) {  // the board's rows; frame rows below stay in place
         const int j = (int)rand_masked(rng, (uint32_t)i);
         const uint64_t a = (idx >> (4 * i)) & 0xFull, b = (idx >> (4 * j)) & 0xFull;
         idx &= ~((0xFull << (4 * i)) | (0xFull << (4 * j)));
@@ -739,23 +935,25 @@ M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng) {
 // --------------------------------------------------------------------------
 template <class CF, class RNG, class Store>
 M3_HD bool apply_begin(typename CF::Bd* P, int n_actions, int action, RNG& rng, uint32_t& flags,
-                       typename CF::Bd& HL, typename CF::Bd& VL, Store& st, int& reward, bool legal_now = true) {
+                       typename CF::Bd& HL, typename CF::Bd& VL, Store& st, int& reward,
+                       const typename CF::Dim& dm = typename CF::Dim{}) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
-    constexpr int C = CF::C, R = CF::R, TM = CF::TM;
+    constexpr int C = CF::C, TM = CF::TM;  // C: the row stride of the bit layout
     constexpr int H = CF::H, V = CF::V, B = CF::B, M = CF::M;
-    constexpr Bd VALID = G::valid();
+    const int R = dm.rows(), CB = dm.cols();  // the board (== R, C unless in a frame)
+    const Bd VALID = dm.valid();
     flags = 0u;
     reward = 0;
     mark<PH_LOAD>(st);
-    if (n_actions < 1 || action < 0 || action >= CF::A) {      // :44-45, KeyError at :48
+    if (n_actions < 1 || action < 0 || action >= dm.actions()) {  // :44-45, KeyError at :48
         flags = (n_actions < 1) ? FLAG_TERMINAL : FLAG_BAD_ACTION;
-        if (legal_now) legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL);  // else: the caller's
+        legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL, dm);
         return false;
     }
     rng.reseed();                                               // :46
     // decode (boardConfig.py:45-59)
-    constexpr int AR = 2 * C - 1, BR = C - 1;
+    const int AR = 2 * CB - 1, BR = CB - 1;
     int sr, sc, tr, tc;
     if (action % AR >= BR) {
         sc = action % AR - BR;
@@ -788,11 +986,11 @@ M3_HD bool apply_begin(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
         zr = Bd::zero();  // :84-103 select TB == max(token1, token2) == M: empty by construction
     } else if (are(B, B)) {                                     // :112-116
         const int r0 = tr - 2 < 0 ? 0 : tr - 2, r1 = tr + 2 > R ? R : tr + 2;
-        const int c0 = tc - 2 < 0 ? 0 : tc - 2, c1 = tc + 2 > C ? C : tc + 2;
+        const int c0 = tc - 2 < 0 ? 0 : tc - 2, c1 = tc + 2 > CB ? CB : tc + 2;
         zr = G::row_band(r0, r1) & G::col_band(c0, c1);
     } else if (are(B, H) || are(B, V)) {                        // :123-125
         const int r0 = tr - 2 < 0 ? 0 : tr - 2, r1 = tr + 2 > R ? R : tr + 2;
-        const int c0 = tc - 2 < 0 ? 0 : tc - 2, c1 = tc + 2 > C ? C : tc + 2;
+        const int c0 = tc - 2 < 0 ? 0 : tc - 2, c1 = tc + 2 > CB ? CB : tc + 2;
         zr = G::col_band(c0, c1) | G::row_band(r0, r1);
     } else if (are(H, V)) {                                     // :130-132 rows < t.col, rows >= t.row
         zr = G::row_band(0, tc < R ? tc : R) | G::row_band(tr, R);
@@ -807,7 +1005,7 @@ M3_HD bool apply_begin(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
     mark<PH_SWAP>(st);
     // first pass with all 7 planes (input values may exceed 32 until the clip)
     Bd z = zr | VALID.andnot(tb_nonzero<CF>(P));
-    z = fire_specials<CF, CF::NP>(P, z);
+    z = fire_specials<CF, CF::NP>(P, z, dm);  // (in a frame: also clips the windows above to the board)
     reward += score<CF, CF::NP>(P, z);
     merge_clip<CF, CF::NP>(P, z, sw);
     mark<PH_CLEAR>(st);
@@ -831,10 +1029,10 @@ enum : int { CASX_STOP_SETTLED = 1, CASX_STOP_DEAD = 2 };
 
 template <class CF, int OPTS, class RNG, class Store>
 M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typename CF::Bd& HL,
-                           typename CF::Bd& VL, Store& st, int& reward, int limit, bool start_settled) {
+                           typename CF::Bd& VL, Store& st, int& reward, int limit, bool start_settled,
+                           const typename CF::Dim& dm = typename CF::Dim{}) {
     using Bd = typename CF::Bd;
-    using G = typename CF::G;
-    constexpr Bd VALID = G::valid();
+    const Bd VALID = dm.valid();
     Bd sw[3];
     int it = 0;
     bool settled = start_settled;
@@ -844,10 +1042,14 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
         if (!settled) {
             for (;;) {  // cascade: refill, rematch, clear while matches remain
                 if (it == limit) return CAS_PAUSED;             // paused before iteration limit + 1
+                if (it >= CASCADE_CAP) {
+                    flags |= FLAG_CASCADE_CAP;
+                    break;
+                }
                 ++it;
-                const Bd em = gravity<CF>(P);                   // :166-173
+                const Bd em = gravity<CF>(P, dm);               // :166-173
                 mark<PH_DROP>(st);
-                refill<CF>(P, em, rng);
+                refill<CF>(P, em, rng, dm);
                 mark<PH_REFILL>(st);
                 if (rng.overflow) break;
                 const int mr = get_matches<CF>(P, mask, sw, st);  // :176-181
@@ -858,7 +1060,7 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
                 }
                 if (mr != MATCH_FOUND) break;
                 Bd z = mask | VALID.andnot(tb_nonzero<CF>(P));  // :199 + TB==0 cells
-                z = fire_specials<CF, 6>(P, z);
+                z = fire_specials<CF, 6>(P, z, dm);
                 reward += score<CF, 6>(P, z);
                 merge_clip<CF, 6>(P, z, sw);
                 mark<PH_CLEAR>(st);
@@ -869,7 +1071,7 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
         settled = false;
         // no match left: the legal set of the settled board, computed once
         // after the (divergent) cascade so the wave runs it once
-        legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
+        legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL, dm);
         mark<PH_LEGAL>(st);
         if (HL.any() || VL.any()) break;
         if constexpr ((OPTS & CASX_STOP_DEAD) != 0) return CAS_DEAD;
@@ -879,7 +1081,7 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
                 flags |= FLAG_SHUFFLE_CAP;
                 break;
             }
-            shuffle_rows<CF>(P, rng);
+            shuffle_rows<CF>(P, rng, dm);
             flags |= FLAG_SHUFFLED;
             ++shuffles;
             const int mr = get_matches<CF>(P, mask, sw, st);
@@ -888,11 +1090,11 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
                 return CAS_DONE;
             }
             found = mr == MATCH_FOUND;
-            if (!found) legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL);
+            if (!found) legal_masks<CF>(P, special_mask<CF, 6>(P), HL, VL, dm);
         }
         if (!found) break;                                      // :195-196
         Bd z = mask | VALID.andnot(tb_nonzero<CF>(P));         // :199 + TB==0 cells
-        z = fire_specials<CF, 6>(P, z);
+        z = fire_specials<CF, 6>(P, z, dm);
         reward += score<CF, 6>(P, z);
         merge_clip<CF, 6>(P, z, sw);
         mark<PH_CLEAR>(st);
@@ -905,8 +1107,9 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
 // false when paused (see apply_begin)
 template <class CF, class RNG, class Store>
 M3_HD bool apply_cascade(typename CF::Bd* P, RNG& rng, uint32_t& flags, typename CF::Bd& HL,
-                         typename CF::Bd& VL, Store& st, int& reward, int limit) {
-    return apply_cascade_ex<CF, 0>(P, rng, flags, HL, VL, st, reward, limit, false) != CAS_PAUSED;
+                         typename CF::Bd& VL, Store& st, int& reward, int limit,
+                         const typename CF::Dim& dm = typename CF::Dim{}) {
+    return apply_cascade_ex<CF, 0>(P, rng, flags, HL, VL, st, reward, limit, false, dm) != CAS_PAUSED;
 }
 
 // A paused cascade's live state as Cont<CF, RNG>::WORDS 32-bit words: planes
@@ -951,10 +1154,11 @@ struct Cont {
 // Returns the step reward (0 when flags ask for a recompute).
 template <class CF, class RNG, class Store>
 M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, uint32_t& flags,
-                       typename CF::Bd& HL, typename CF::Bd& VL, Store& st) {
+                       typename CF::Bd& HL, typename CF::Bd& VL, Store& st,
+                       const typename CF::Dim& dm = typename CF::Dim{}) {
     int reward;
-    if (apply_begin<CF>(P, n_actions, action, rng, flags, HL, VL, st, reward))
-        apply_cascade<CF>(P, rng, flags, HL, VL, st, reward, -1);
+    if (apply_begin<CF>(P, n_actions, action, rng, flags, HL, VL, st, reward, dm))
+        apply_cascade<CF>(P, rng, flags, HL, VL, st, reward, -1, dm);
     return (flags & FLAG_RECOMPUTE) ? 0 : reward;
 }
 
@@ -963,25 +1167,28 @@ M3_HD int apply_action(typename CF::Bd* P, int n_actions, int action, RNG& rng, 
 // seeded. Writes the planes (values 1..T).
 // --------------------------------------------------------------------------
 template <class CF, class RNG, class S>
-M3_HD void init_board(typename CF::Bd* P, RNG& mt, S& st) {
+M3_HD void init_board(typename CF::Bd* P, RNG& mt, S& st, const typename CF::Dim& dm = typename CF::Dim{}) {
     using Bd = typename CF::Bd;
 #pragma unroll
     for (int p = 0; p < CF::NP; ++p) P[p] = Bd::zero();
+    const int RB = dm.rows(), CB = dm.cols();
+    const uint32_t tmask = dm.tile_mask(), trng = dm.tile_rng();
     // randint(1, T+1, (R, C)) fills cells in row-major order; as in the
     // refill, one raw draw per loop trip so lanes never wait on each other's
-    // rejections. `take` = the value was accepted and belongs to cell x.
+    // rejections. An accepted value belongs to cell (r, c).
     auto fill = [&](const Bd* only) {
-        int x = 0;
-        while (x < CF::N) {
-            uint32_t v = 1u;
-            if constexpr (CF::TILE_RNG != 0u) {
-                v = mt.next32() & CF::TILE_MASK;
-                if (mt.overflow) return;
-                if (v > CF::TILE_RNG) continue;
-                v += 1u;
-            }
+        int r = 0, c = 0;
+        while (r < RB) {
+            uint32_t v = mt.next32() & tmask;
+            if (mt.overflow) return;
+            if (v > trng) continue;
+            v += 1u;
+            const int x = r * CF::C + c;
             if (!only || only->test(x)) set_cell<CF, CF::BITS>(P, x, (int)v);
-            ++x;
+            if (++c == CB) {
+                c = 0;
+                ++r;
+            }
         }
     };
     mark<PH_LOAD>(st);
@@ -998,11 +1205,6 @@ M3_HD void init_board(typename CF::Bd* P, RNG& mt, S& st) {
     }
 }
 
-template <class CF, class RNG>
-M3_HD void init_board(typename CF::Bd* P, RNG& mt) {
-    NoStore ns;
-    init_board<CF>(P, mt, ns);
-}
 
 // --------------------------------------------------------------------------
 // BoardV2.__init__ (boardv2.py:17-27) on a tile stream: every round of the
@@ -1038,6 +1240,7 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
     using G = typename CF::G;
     constexpr int TW = TileGen<CF>::TWMAX, N = CF::N, MAXR = TileGen<CF>::MAXR;
     constexpr Bd VALID = G::valid();
+    static_assert(!CF::DYN, "frame boards reset on FullMT (k_init_fix_lane)");
     static_assert(CF::TILE_RNG > 0u, "randint(1, 2) consumes no draws");
     uint32_t cur[CF::BITS];
 #pragma unroll
@@ -1189,6 +1392,92 @@ M3_HD void words_from_planes(const typename CF::Bd* P, uint32_t* cw) {
         transpose8(lo, hi);
         if (2 * g < NW) cw[2 * g] = lo;
         if (2 * g + 1 < NW) cw[2 * g + 1] = hi;
+    }
+}
+
+
+// --------------------------------------------------------------------------
+// Frame boards (FCfg) <-> the board's own int8 cells (R*C bytes, row-major,
+// any alignment): board row r is C bytes, cells (r, 0..C-1) sit at frame
+// bits r*16 .. r*16 + C-1; two 8x8 transposes per row.
+// --------------------------------------------------------------------------
+template <class CF>
+M3_HD void frame_from_bytes(const uint8_t* src, typename CF::Bd* P, const typename CF::Dim& dm) {
+    static_assert(CF::DYN && CF::C == 16, "frame layout");
+    const int RB = dm.rows(), CB = dm.cols();
+#pragma unroll
+    for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+#pragma unroll
+    for (int r = 0; r < CF::R; ++r) {
+        if (r < RB) {
+            const uint8_t* row = src + r * CB;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < CB) w[k >> 2] |= (uint32_t)row[k] << (8 * (k & 3));
+            transpose8(w[0], w[1]);
+            transpose8(w[2], w[3]);
+#pragma unroll
+            for (int p = 0; p < CF::NP; ++p) {
+                const uint32_t b0 = (w[p < 4 ? 0 : 1] >> (8 * (p & 3))) & 0xFFu;
+                const uint32_t b1 = (w[p < 4 ? 2 : 3] >> (8 * (p & 3))) & 0xFFu;
+                P[p].w[r >> 1] |= (b0 | (b1 << 8)) << ((r & 1) * 16);
+            }
+        }
+    }
+}
+
+template <class CF>
+M3_HD void frame_to_bytes(const typename CF::Bd* P, uint8_t* dst, const typename CF::Dim& dm) {
+    static_assert(CF::DYN && CF::C == 16, "frame layout");
+    const int RB = dm.rows(), CB = dm.cols();
+#pragma unroll
+    for (int r = 0; r < CF::R; ++r) {
+        if (r < RB) {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int p = 0; p < CF::NP; ++p) {
+                const uint32_t bits = (P[p].w[r >> 1] >> ((r & 1) * 16)) & 0xFFFFu;
+                w[p < 4 ? 0 : 1] |= (bits & 0xFFu) << (8 * (p & 3));
+                w[p < 4 ? 2 : 3] |= (bits >> 8) << (8 * (p & 3));
+            }
+            transpose8(w[0], w[1]);
+            transpose8(w[2], w[3]);
+            uint8_t* row = dst + r * CB;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < CB) row[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+
+// One round of BoardV2.__init__ on a frame board (boardv2.py:21 / :25):
+// randint(1, T+1, (R, C)) draws a tile for EVERY cell in row-major order;
+// cells outside `only` take their draw and drop it (array[mask] = new[mask]).
+template <class CF, class RNG>
+M3_HD void fill_round_frame(typename CF::Bd* P, RNG& mt, const typename CF::Bd* only, const typename CF::Dim& dm) {
+    const int RB = dm.rows(), CB = dm.cols();
+    const uint32_t tmask = dm.tile_mask(), trng = dm.tile_rng(), rowm = (1u << CB) - 1u;
+#pragma unroll
+    for (int r = 0; r < CF::R; ++r) {
+        if (r < RB) {
+            uint32_t t[CF::BITS];
+#pragma unroll
+            for (int p = 0; p < CF::BITS; ++p) t[p] = 0u;
+            for (int c = 0; c < CB; ++c) {
+                uint32_t v;
+                do {
+                    v = mt.next32() & tmask;
+                } while (v > trng);
+                v += 1u;
+#pragma unroll
+                for (int p = 0; p < CF::BITS; ++p) t[p] |= ((v >> p) & 1u) << c;
+            }
+            const int sh = (r & 1) * 16;
+            const uint32_t m = (only ? (only->w[r >> 1] >> sh) & rowm : rowm) << sh;
+#pragma unroll
+            for (int p = 0; p < CF::BITS; ++p) P[p].w[r >> 1] = (P[p].w[r >> 1] & ~m) | ((t[p] << sh) & m);
+        }
     }
 }
 

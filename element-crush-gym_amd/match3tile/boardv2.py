@@ -39,6 +39,14 @@ def _ctx(cfg: BoardConfig) -> _native.Context:
     return _native.context(cfg.rows, cfg.columns, cfg.types)
 
 
+def _ids_past_board(cfg: BoardConfig) -> None:
+    """rows < columns: the last action ids decode to a swap with row `rows` (boardConfig.py:27,45-59),
+    so the reference's legal_actions -- called by every apply_action too (boardv2.py:188) -- raises
+    numpy's IndexError. Same here (the kernels refuse such a shape for anything but a reset)."""
+    if cfg.rows < cfg.columns:
+        raise IndexError(f"index {cfg.rows} is out of bounds for axis 0 with size {cfg.rows}")
+
+
 class BoardV2(State):
     # the reference's default argument is built once, at import (boardv2.py:12)
     def __init__(self, n_actions: int, cfg=BoardConfig(), array: np.ndarray = None):
@@ -57,6 +65,7 @@ class BoardV2(State):
     # ---- State interface -------------------------------------------------------
     @property
     def legal_actions(self) -> List[int]:
+        _ids_past_board(self.cfg)
         if len(self._actions) == 0:                          # cached only while non-empty
             self._actions = _ctx(self.cfg).legal_actions(self.array)
         return self._actions
@@ -73,6 +82,9 @@ class BoardV2(State):
         if action not in self.cfg.actions:                   # reseed happens before the KeyError
             np.random.seed(self.cfg.seed)
             raise KeyError(action)
+        if self.cfg.rows < self.cfg.columns:
+            np.random.seed(self.cfg.seed)
+            _ids_past_board(self.cfg)
         res = _ctx(self.cfg).apply_actions(self.array, int(self.cfg.seed) & 0xFFFFFFFF, self.n_actions,
                                            int(action))
         _sync_global_rng(self.cfg.seed, int(res["draws"][0]))

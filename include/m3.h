@@ -48,6 +48,7 @@ extern "C" {
 #define M3_FLAG_SHUFFLE_CAP 0x04u /* dead-board shuffle cycled past the cap: reference hangs (boardv2.py:188-194) */
 #define M3_FLAG_NO_LEGAL 0x08u    /* no legal action to sample: reference raises in np.random.choice */
 #define M3_FLAG_SHUFFLED 0x10u    /* the dead-board shuffle ran */
+#define M3_FLAG_CASCADE_CAP 0x100u /* cascade stopped after 1024 refills: the reference keeps going (types = 2 boards) */
 
 typedef struct m3_ctx m3_ctx;
 typedef struct m3_env m3_env;

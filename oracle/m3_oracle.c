@@ -523,6 +523,13 @@ int64_t m3o_apply_action(const m3o_cfg *cfg, uint32_t seed, int n_actions,
 }
 
 /* ---- seeded random episode (samplerTasks.py:9-14 + env.py:48-56 bookkeeping) */
+/* Shuffle cap of the episode / rollout drivers below. The reference has none
+ * (a cycling dead board hangs it, boardv2.py:188-194); the default 2^20 is
+ * "never" for boards that terminate. Tests on tiny boards, where cycling dead
+ * boards are common, lower it to the GPU's 1024 and compare the flag. */
+static int g_episode_cap = 1 << 20;
+void m3o_set_episode_shuffle_cap(int cap) { g_episode_cap = cap; }
+
 int m3o_random_episode(const m3o_cfg *cfg, uint32_t seed, int num_moves, int env_goal,
                        int32_t *actions, int32_t *rewards, int32_t *draws,
                        uint8_t *done, int32_t *final_board, int *flags) {
@@ -542,7 +549,7 @@ int m3o_random_episode(const m3o_cfg *cfg, uint32_t seed, int num_moves, int env
         if (nl == 0) { *flags |= M3O_FLAG_NO_LEGAL; break; }              /* choice([]) raises */
         int act = legal[m3o_randint(&mt, 0, nl)];                          /* samplerTasks.py:13 */
         int f = 0;
-        int64_t r = m3o_apply_action(cfg, seed, n_actions, a, act, b, &mt, &f, 1 << 20);
+        int64_t r = m3o_apply_action(cfg, seed, n_actions, a, act, b, &mt, &f, g_episode_cap);
         *flags |= f;
         n_actions--;
         memcpy(a, b, sizeof(int32_t) * (size_t)N);
@@ -596,7 +603,7 @@ int64_t m3o_rollout(const m3o_cfg *cfg, const int32_t *board, uint32_t seed, int
         if (nl == 0) { *flags |= M3O_FLAG_NO_LEGAL; break; }               /* choice([]) raises */
         int act = legal[m3o_randint(&mt, 0, nl)];                           /* mcts.py:17 */
         int f = 0;
-        gain += m3o_apply_action(cfg, seed, n_actions, a, act, b, &mt, &f, 1 << 20);  /* mcts.py:18 */
+        gain += m3o_apply_action(cfg, seed, n_actions, a, act, b, &mt, &f, g_episode_cap);  /* mcts.py:18 */
         *flags |= f;
         n_actions--;
         (*steps)++;

@@ -71,6 +71,7 @@ int64_t m3o_apply_action(const m3o_cfg *cfg, uint32_t seed, int n_actions,
  * Match3Env bookkeeping (env.py:48-56): init, reseed, then per move
  * choice(legal) -> apply_action. Writes per-move actions/rewards/draws and the
  * final board. Returns number of moves executed. */
+void m3o_set_episode_shuffle_cap(int cap);
 int m3o_random_episode(const m3o_cfg *cfg, uint32_t seed, int num_moves, int env_goal,
                        int32_t *actions, int32_t *rewards, int32_t *draws,
                        uint8_t *done, int32_t *final_board, int *flags);

@@ -73,6 +73,7 @@ def lib():
         L.m3o_apply_action.argtypes = [P(Cfg), ctypes.c_uint32, ctypes.c_int, i32p, ctypes.c_int,
                                        i32p, P(MT), P(ctypes.c_int), ctypes.c_int]
         L.m3o_apply_action.restype = ctypes.c_int64
+        L.m3o_set_episode_shuffle_cap.argtypes = [ctypes.c_int]
         L.m3o_random_episode.argtypes = [P(Cfg), ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
                                          i32p, i32p, i32p, u8p, i32p, P(ctypes.c_int)]
         L.m3o_random_episode.restype = ctypes.c_int
@@ -96,7 +97,10 @@ def _p(a, ct):
 class Oracle:
     """Python face of the C oracle for one board shape."""
 
-    def __init__(self, rows=9, columns=9, types=6, shuffle_cap=1024):
+    def __init__(self, rows=9, columns=9, types=6, shuffle_cap=1024, episode_shuffle_cap=1 << 20):
+        """shuffle_cap: apply_action's (the GPU's 1024); episode_shuffle_cap: the episode / rollout
+        drivers' (default: effectively none, like the reference)."""
+        self.episode_shuffle_cap = episode_shuffle_cap
         self.cfg = Cfg()
         lib().m3o_cfg_init(ctypes.byref(self.cfg), rows, columns, types)
         self.R, self.C, self.T = rows, columns, types
@@ -154,6 +158,7 @@ class Oracle:
         done = np.zeros(num_moves, np.uint8)
         fb = np.zeros((self.R, self.C), np.int32)
         flags = ctypes.c_int()
+        lib().m3o_set_episode_shuffle_cap(self.episode_shuffle_cap)
         n = lib().m3o_random_episode(ctypes.byref(self.cfg), seed & 0xFFFFFFFF, num_moves, env_goal,
                                      _p(acts, ctypes.c_int32), _p(rews, ctypes.c_int32), _p(drw, ctypes.c_int32),
                                      _p(done, ctypes.c_uint8), _p(fb, ctypes.c_int32), ctypes.byref(flags))
@@ -172,6 +177,7 @@ class Oracle:
         final = np.zeros((n, self.R * self.C), np.int32)
         moves = np.zeros(n, np.int32)
         flags = np.zeros(n, np.int32)
+        lib().m3o_set_episode_shuffle_cap(self.episode_shuffle_cap)
         lib().m3o_batch_episodes(ctypes.byref(self.cfg), n, _p(seeds, ctypes.c_uint32), num_moves, env_goal, threads,
                                  _p(acts, ctypes.c_int32), _p(rews, ctypes.c_int32), _p(drw, ctypes.c_int32),
                                  _p(done, ctypes.c_uint8), _p(final, ctypes.c_int32), _p(moves, ctypes.c_int32),
@@ -191,6 +197,7 @@ class Oracle:
         draws = np.zeros(n, np.int64)
         flags = np.zeros(n, np.int32)
         final = np.zeros((n, self.R * self.C), np.int32)
+        lib().m3o_set_episode_shuffle_cap(self.episode_shuffle_cap)
         lib().m3o_batch_rollouts(ctypes.byref(self.cfg), n, _p(boards, ctypes.c_int32), _p(seeds, ctypes.c_uint32),
                                  _p(n_actions, ctypes.c_int32), _p(rollout_seeds, ctypes.c_uint32), threads,
                                  _p(gain, ctypes.c_int32), _p(steps, ctypes.c_int32), _p(draws, ctypes.c_int64),
@@ -200,6 +207,7 @@ class Oracle:
     def run_episodes(self, seeds, num_moves=20, env_goal=2**31 - 1, threads=1):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
         tot = np.zeros(len(seeds), dtype=np.int64)
+        lib().m3o_set_episode_shuffle_cap(self.episode_shuffle_cap)
         steps = lib().m3o_run_episodes(ctypes.byref(self.cfg), len(seeds), _p(seeds, ctypes.c_uint32),
                                        num_moves, env_goal, threads, _p(tot, ctypes.c_int64))
         return int(steps), tot

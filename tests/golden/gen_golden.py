@@ -21,6 +21,10 @@ Files written:
   env.npz         Match3Env runs of the README.md:18-31 loop (env.board.random_action(), step,
                   reset at done with and without a seed), bookkeeping restated over the reference
                   BoardV2 (env.py cannot run at the snapshot): obs/reward/done/truncated per step
+  shapes.npz      init / legal / steps / episodes for BoardConfigs other than 9x9x6 and 16x16x8
+                  (square, rows > columns, columns = 3 -- the decode quirk -- and few types), and
+                  for rows < columns, where the reference's legal_actions / apply_action raise
+                  IndexError, the init boards plus that error
 """
 from __future__ import annotations
 
@@ -42,6 +46,14 @@ from match3tile.boardv2 import BoardV2  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 SHAPES = [(9, 9, 6), (16, 16, 8)]
+
+
+class _Timeout(Exception):
+    pass
+
+
+def _alarm(signum, frame):
+    raise _Timeout()
 
 
 def raw(n):
@@ -194,7 +206,20 @@ def gen_init(pool):
 
 # ---------------------------------------------------------------------- episodes
 def _episode(args):
-    """samplerTasks.random_task (samplerTasks.py:9-14) with a fixed seed."""
+    """samplerTasks.random_task (samplerTasks.py:9-14) with a fixed seed (None if the reference
+    hangs in a cycling dead-board shuffle, boardv2.py:188-194, or raises in np.random.choice([])
+    on a board without a legal action -- both possible on tiny boards)."""
+    signal.signal(signal.SIGALRM, _alarm)
+    signal.alarm(5)
+    try:
+        return _episode_body(args)
+    except (_Timeout, ValueError):  # ValueError: np.random.choice([]) -- a board with no legal action
+        return None
+    finally:
+        signal.alarm(0)
+
+
+def _episode_body(args):
     R, C, T, seed, moves = args
     cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
     state = BoardV2(moves, cfg)
@@ -271,6 +296,19 @@ class _RefEnv:
 
 
 def _env_run(args):
+    """None where the reference crashes (no legal action: np.random.choice([])) or hangs (a cycling
+    dead-board shuffle) -- tiny boards only; gen_env keeps the runs that complete."""
+    signal.signal(signal.SIGALRM, _alarm)
+    signal.alarm(20)
+    try:
+        return _env_run_body(args)
+    except (_Timeout, ValueError):
+        return None
+    finally:
+        signal.alarm(0)
+
+
+def _env_run_body(args):
     """The README.md:18-31 loop: action = env.board.random_action() (= np.random.choice(
     board.legal_actions) from numpy's global stream, samplerTasks.py:13), step, reset at done
     with the next entry of `resets` (-1: reset() without a seed, the env.py:62 quirk)."""
@@ -299,17 +337,30 @@ def _env_run(args):
     return out
 
 
+# shapes beyond the two headline ones (rows, columns, types): square, rows > columns,
+# columns = 3 (boardConfig.py:50's literal 3 sends the vertical ids of row r to row r - 1),
+# three types, fifteen types
+EXTRA_SHAPES = [(7, 7, 4), (8, 8, 5), (10, 8, 5), (5, 3, 3), (12, 12, 7), (16, 3, 4), (6, 5, 15), (3, 3, 3)]
+# rows < columns: BoardV2.__init__ works, legal_actions / apply_action raise IndexError
+WIDE_SHAPES = [(8, 10, 5), (3, 5, 3)]
+
+
 def gen_env(pool, shapes=None):
     rng = np.random.default_rng(2024)
     out = {}
     plan = [(20, 500), (20, 150), (7, 10**9), (12, 300)]
-    for (R, C, T), n_runs, n_steps in shapes or [((9, 9, 6), 48, 60), ((16, 16, 8), 16, 45)]:
+    # (tiny or many-type boards where most README runs hit a board without a legal move are left out)
+    extra = [((R, C, T), 6, 30) for (R, C, T) in EXTRA_SHAPES if (R, C, T) not in ((3, 3, 3), (6, 5, 15))]
+    for (R, C, T), n_runs, n_steps in shapes or [((9, 9, 6), 48, 60), ((16, 16, 8), 16, 45)] + extra:
         args = []
-        for i in range(n_runs):
+        for i in range(2 * n_runs):
             moves, goal = plan[i % len(plan)]
             resets = [int(rng.integers(1, 2**32 - 1)) if rng.random() < 0.5 else -1 for _ in range(8)]
             args.append((R, C, T, int(rng.integers(1, 2**32 - 1)), moves, goal, n_steps, resets))
         res = pool.map(_env_run, args, chunksize=2)
+        keep = [i for i, r in enumerate(res) if r is not None][:n_runs]
+        assert len(keep) == n_runs, (R, C, T, len(keep))
+        args, res = [args[i] for i in keep], [res[i] for i in keep]
         tag = f"{R}x{C}x{T}"
         out[f"seed_{tag}"] = np.array([a[3] for a in args], dtype=np.uint32)
         out[f"moves_{tag}"] = np.array([a[4] for a in args], dtype=np.int32)
@@ -325,6 +376,20 @@ def gen_env(pool, shapes=None):
 
 # ------------------------------------------------------------------------- steps
 def _step_case(args):
+    """(next board, reward, draws, n_actions) of one apply_action; draws -2 if the reference hangs
+    (a cycling dead-board shuffle, boardv2.py:188-194)."""
+    signal.signal(signal.SIGALRM, _alarm)
+    signal.alarm(3)
+    try:
+        return _step_case_body(args)
+    except _Timeout:
+        R, C = args[0], args[1]
+        return np.zeros((R, C), np.int8), 0, -2, 0
+    finally:
+        signal.alarm(0)
+
+
+def _step_case_body(args):
     R, C, T, board, seed, n_actions, action = args
     cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
     st = BoardV2(int(n_actions), cfg, np.array(board, dtype=np.int64))
@@ -347,14 +412,23 @@ def step_cases(R, C, T, rng, n_play=1500):
     cases = []
     # boards from seeded play
     play = []
+    signal.signal(signal.SIGALRM, _alarm)
     for s in range(1, 120):
         c2 = BoardConfig(seed=s, rows=R, columns=C, types=T)
         b = BoardV2(20, c2)
         np.random.seed(s)
-        for _ in range(6):
-            play.append((b.array.copy(), s))
-            la = b.legal_actions
-            b = b.apply_action(int(np.random.choice(la)))
+        signal.alarm(3)  # tiny boards: the reference can cycle forever in the dead-board shuffle
+        try:
+            for _ in range(6):
+                play.append((b.array.copy(), s))
+                la = b.legal_actions
+                if not la:
+                    break
+                b = b.apply_action(int(np.random.choice(la)))
+        except _Timeout:
+            pass
+        finally:
+            signal.alarm(0)
     for i in range(n_play):
         board, s = play[rng.integers(0, len(play))]
         board = board.copy()
@@ -449,14 +523,6 @@ def gen_legal():
 
 
 # ----------------------------------------------------------------------- shuffle
-class _Timeout(Exception):
-    pass
-
-
-def _alarm(signum, frame):
-    raise _Timeout()
-
-
 def _shuffle_case(args):
     R, C, T, board, seed, action = args
     cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
@@ -496,8 +562,80 @@ def gen_shuffle(pool):
     np.savez_compressed(os.path.join(OUT, "shuffle.npz"), **out)
 
 
+def _wide_case(args):
+    R, C, T, seed = args
+    cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
+    b = BoardV2(20, cfg)
+    d = draws_since_seed(int(seed))  # (before the calls below reseed and raise)
+    errs = []
+    for call in (lambda: b.legal_actions, lambda: b.apply_action(0)):
+        try:
+            call()
+            errs.append("")
+        except Exception as e:  # noqa: BLE001 -- the reference's own exception is the datum
+            errs.append(type(e).__name__)
+    return b.array.astype(np.int8), d, errs
+
+
+def gen_shapes(pool):
+    rng = np.random.default_rng(777)
+    out = {}
+    for (R, C, T) in EXTRA_SHAPES:
+        tag = f"{R}x{C}x{T}"
+        cfg = BoardConfig(seed=1, rows=R, columns=C, types=T)
+        seeds = np.concatenate([np.arange(1, 253), [2**31 - 2, 2**32 - 1, 123456789, 987654321]]).astype(np.uint64)
+        res = pool.map(_init_one, [(R, C, T, s) for s in seeds])
+        out[f"init_seeds_{tag}"] = seeds
+        out[f"init_boards_{tag}"] = np.array([r[0] for r in res])
+        out[f"init_draws_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        # legal sets: init boards, boards with specials / zeros, patterned (near-dead) boards
+        boards = [r[0].astype(np.int64) for r in res[:120]]
+        for _ in range(120):
+            b = rng.integers(1, T + 1, size=(R, C))
+            for _ in range(rng.integers(0, 4)):
+                b[rng.integers(0, R), rng.integers(0, C)] = [cfg.h_line, cfg.v_line, cfg.bomb, cfg.mega_token,
+                                                             0][rng.integers(0, 5)]
+            boards.append(b)
+        for m in range(2, T + 1):
+            for a in range(1, 3):
+                for bb in range(1, 3):
+                    boards.append(np.fromfunction(lambda r, c: (a * r + bb * c) % m + 1, (R, C), dtype=np.int64))
+        out[f"legal_boards_{tag}"] = np.array(boards, dtype=np.int8)
+        out[f"legal_{tag}"] = np.array([legal_bits(cfg, b) for b in boards], dtype=np.uint8)
+        # apply_action transitions (play, specials, typed values, combos, edges, illegal swaps, terminal)
+        cases = step_cases(R, C, T, rng, 400)
+        res = pool.map(_step_case, [(R, C, T, b, s, na, a) for (b, s, na, a) in cases], chunksize=16)
+        out[f"step_board_{tag}"] = np.array([c[0] for c in cases], dtype=np.int8)
+        out[f"step_seed_{tag}"] = np.array([c[1] for c in cases], dtype=np.uint32)
+        out[f"step_n_actions_{tag}"] = np.array([c[2] for c in cases], dtype=np.int32)
+        out[f"step_action_{tag}"] = np.array([c[3] for c in cases], dtype=np.int32)
+        out[f"step_next_{tag}"] = np.array([r[0] for r in res])
+        out[f"step_reward_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        out[f"step_draws_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+        # seeded random_task episodes
+        eseeds = np.arange(1, 81, dtype=np.uint64)
+        res = pool.map(_episode, [(R, C, T, s, 20) for s in eseeds], chunksize=2)
+        keep = [i for i, r in enumerate(res) if r is not None][:64]  # (drop seeds where the reference hangs)
+        eseeds, res = eseeds[keep], [res[i] for i in keep]
+        out[f"ep_seeds_{tag}"] = eseeds
+        out[f"ep_init_{tag}"] = np.array([r[0] for r in res])
+        out[f"ep_actions_{tag}"] = np.array([r[1] for r in res], dtype=np.int16)
+        out[f"ep_rewards_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+        out[f"ep_draws_{tag}"] = np.array([r[3] for r in res], dtype=np.int16)
+        out[f"ep_final_{tag}"] = np.array([r[4][-1] for r in res])
+    for (R, C, T) in WIDE_SHAPES:
+        tag = f"{R}x{C}x{T}"
+        seeds = np.arange(1, 129, dtype=np.uint64)
+        res = pool.map(_wide_case, [(R, C, T, s) for s in seeds])
+        out[f"wide_seeds_{tag}"] = seeds
+        out[f"wide_boards_{tag}"] = np.array([r[0] for r in res])
+        out[f"wide_draws_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        out[f"wide_errors_{tag}"] = np.array(sorted({e for r in res for e in r[2]}))
+    np.savez_compressed(os.path.join(OUT, "shapes.npz"), **out)
+
+
 def main():
-    which = sys.argv[1:] or ["prng", "matches", "legal", "init", "steps", "episodes", "shuffle"]
+    which = sys.argv[1:] or ["prng", "matches", "legal", "init", "steps", "episodes", "shuffle", "env", "shapes"]
     with Pool(8) as pool:
         for w in which:
             print("generating", w, flush=True)
@@ -517,6 +655,8 @@ def main():
                 gen_shuffle(pool)
             elif w == "env":
                 gen_env(pool)
+            elif w == "shapes":
+                gen_shapes(pool)
 
 
 if __name__ == "__main__":

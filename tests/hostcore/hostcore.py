@@ -12,7 +12,7 @@ SRC = [os.path.join(HERE, "hostcore.hip")] + [
     ("m3_rules.hpp", "m3_bitboard.hpp", "m3_rng.hpp")]
 _lib = None
 CFG_ID = {(9, 9, 6): 0, (16, 16, 8): 1}
-AW = {(9, 9, 6): 5, (16, 16, 8): 15}
+FRAME = 2  # any shape in the 16 x 16 frame (hc_set_frame)
 
 
 def build():
@@ -20,7 +20,8 @@ def build():
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
         return
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", "-shared",
-                    "-o", LIB, SRC[0]], check=True)
+                    "-o", LIB + ".tmp", SRC[0]], check=True)
+    os.replace(LIB + ".tmp", LIB)
 
 
 def lib():
@@ -38,11 +39,20 @@ def _p(a):
 
 
 class HostCore:
-    def __init__(self, R=9, C=9, T=6):
+    """frame=None: the specialised config for 9x9x6 / 16x16x8, the frame for any other shape;
+    frame=True forces the frame form (e.g. to run 9x9x6 through it)."""
+
+    def __init__(self, R=9, C=9, T=6, frame=None):
         self.shape = (R, C, T)
-        self.cfg = CFG_ID[(R, C, T)]
+        self.frame = (R, C, T) not in CFG_ID if frame is None else bool(frame)
+        self.cfg = FRAME if self.frame else CFG_ID[(R, C, T)]
         self.N = R * C
-        self.aw = AW[(R, C, T)]
+        self.A = R * (C - 1) * 2
+        self.aw = (self.A + 31) // 32
+
+    def _sel(self):
+        if self.frame:
+            assert lib().hc_set_frame(*self.shape) == 0, self.shape
 
     def apply(self, boards, seeds, n_actions, actions, small=False):
         boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
@@ -53,6 +63,7 @@ class HostCore:
         out = np.zeros_like(boards)
         rew = np.zeros(n, np.int32); drw = np.zeros(n, np.int32); flg = np.zeros(n, np.int32)
         legal = np.zeros((n, self.aw), np.uint32); nxt = np.zeros(n, np.int32)
+        self._sel()
         self.recomputed = lib().hc_apply(self.cfg, ctypes.c_long(n), _p(boards), _p(seeds), _p(na), _p(acts),
                                          _p(out), _p(rew), _p(drw), _p(flg), _p(legal), _p(nxt), int(small))
         return out, rew, drw, flg, legal, nxt
@@ -62,12 +73,14 @@ class HostCore:
         n = len(seeds)
         out = np.zeros((n, self.N), np.int8); drw = np.zeros(n, np.int32)
         m397 = np.zeros(n, np.uint32); fa = np.zeros(n, np.int32)
+        self._sel()
         self.recomputed = lib().hc_init(self.cfg, ctypes.c_long(n), _p(seeds), _p(out), _p(drw), _p(m397), _p(fa))
         return out, drw, m397, fa
 
     def legal(self, boards):
         boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
         out = np.zeros((len(boards), self.aw), np.uint32)
+        self._sel()
         lib().hc_legal(self.cfg, ctypes.c_long(len(boards)), _p(boards), _p(out))
         return out
 
@@ -75,14 +88,25 @@ class HostCore:
         tbs = np.ascontiguousarray(tbs, dtype=np.int8).reshape(-1, self.N)
         n = len(tbs)
         mask = np.zeros((n, self.N), np.uint8); sp = np.zeros((n, self.N), np.int32); fd = np.zeros(n, np.int32)
+        self._sel()
         lib().hc_matches(self.cfg, ctypes.c_long(n), _p(tbs), _p(mask), _p(sp), _p(fd))
         return mask, sp, fd
 
     def roundtrip(self, boards):
         boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
         out = np.zeros_like(boards)
+        self._sel()
         lib().hc_roundtrip(self.cfg, ctypes.c_long(len(boards)), _p(boards), _p(out))
         return out
+
+
+    def init_scalar(self, seeds):
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        n = len(seeds)
+        out = np.zeros((n, self.N), np.int8); drw = np.zeros(n, np.int32)
+        self._sel()
+        lib().hc_init_scalar(self.cfg, ctypes.c_long(n), _p(seeds), _p(out), _p(drw))
+        return out, drw
 
 
 def bits_to_list(words, A):

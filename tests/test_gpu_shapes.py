@@ -1,0 +1,155 @@
+"""Every other BoardConfig through the same C-ABI: the frame kernels (FCfg, m3_rules.hpp).
+
+Reference fixtures (tests/golden/shapes.npz, gen_golden.py: gen_shapes) for square boards,
+rows > columns, columns = 3 (boardConfig.py:50's literal 3 sends vertical ids of row r to row
+r - 1), three and fifteen tile types; the oracle for large batches; and rows < columns, where
+the reference resets fine but its legal_actions / apply_action raise IndexError."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from match3tile import _native  # noqa: E402
+from match3tile.batched import BatchedMatch3Env  # noqa: E402
+from oracle import Oracle  # noqa: E402
+
+BIG = 2**31 - 1
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if _native.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+
+
+def _tags(g, prefix):
+    return sorted({k[len(prefix):] for k in g.files if k.startswith(prefix)})
+
+
+def _shape(tag):
+    return tuple(int(x) for x in tag.split("x"))
+
+
+def unpack(words, A):
+    return np.unpackbits(np.ascontiguousarray(words, dtype="<u4").view(np.uint8), axis=-1, bitorder="little")[..., :A]
+
+
+def test_fixture_covers_the_asked_shapes(golden):
+    g = golden("shapes")
+    tags = _tags(g, "init_seeds_")
+    for t in ("7x7x4", "8x8x5", "10x8x5", "5x3x3", "12x12x7"):
+        assert t in tags
+    assert set(_tags(g, "wide_seeds_")) == {"8x10x5", "3x5x3"}
+
+
+def test_frame_shapes_golden(golden):
+    g = golden("shapes")
+    for tag in _tags(g, "init_seeds_"):
+        R, C, T = _shape(tag)
+        ctx = _native.Context(R, C, T)
+        A = ctx.A
+        boards, draws, _ = ctx.init_boards(g["init_seeds_" + tag].astype(np.uint32))
+        assert (boards == g["init_boards_" + tag]).all(), tag
+        assert (draws == g["init_draws_" + tag]).all(), tag
+        bits = unpack(ctx.legal_bits(g["legal_boards_" + tag]), A)
+        assert (bits == g["legal_" + tag]).all(), tag
+        ok = g["step_draws_" + tag] != -2  # (-2: the reference hangs in a cycling shuffle)
+        r = ctx.apply_actions(g["step_board_" + tag][ok], g["step_seed_" + tag][ok], g["step_n_actions_" + tag][ok],
+                              g["step_action_" + tag][ok])
+        assert (r["boards"] == g["step_next_" + tag][ok]).all(), tag
+        assert (r["reward"] == g["step_reward_" + tag][ok]).all(), tag
+        live = g["step_draws_" + tag][ok] >= 0
+        assert (r["draws"][live] == g["step_draws_" + tag][ok][live]).all(), tag
+        # seeded random_task episodes through the batched env (its step / reset / random-action kernels)
+        seeds = g["ep_seeds_" + tag].astype(np.uint32)
+        env = BatchedMatch3Env(len(seeds), R, C, T, num_moves=20, env_goal=BIG, seeds=seeds, autoreset=False)
+        assert (env.observations() == g["ep_init_" + tag]).all(), tag
+        for m in range(20):
+            assert (env.next_actions() == g["ep_actions_" + tag][:, m]).all(), (tag, m)
+            env.step()
+            assert (env.rewards() == g["ep_rewards_" + tag][:, m]).all(), (tag, m)
+            assert (env.draws() == g["ep_draws_" + tag][:, m]).all(), (tag, m)
+        assert (env.observations() == g["ep_final_" + tag]).all(), tag
+        env.close()
+        ctx.close()
+
+
+def test_rows_below_columns_reset_but_do_not_step(golden):
+    """rows < columns: BoardV2.__init__ as the reference; legal_actions / apply_action raise IndexError
+    there (and here) -- the C-ABI refuses them with M3_ERR_INVALID."""
+    from match3tile.boardConfig import BoardConfig
+    from match3tile.boardv2 import BoardV2
+    from match3tile.env import Match3Env
+
+    g = golden("shapes")
+    for tag in _tags(g, "wide_seeds_"):
+        R, C, T = _shape(tag)
+        assert list(g["wide_errors_" + tag]) == ["IndexError"]
+        ctx = _native.Context(R, C, T)
+        boards, draws, _ = ctx.init_boards(g["wide_seeds_" + tag].astype(np.uint32))
+        assert (boards == g["wide_boards_" + tag]).all() and (draws == g["wide_draws_" + tag]).all()
+        with pytest.raises(_native.M3Error) as e:
+            ctx.legal_bits(boards[:1])
+        assert e.value.code == -1
+        with pytest.raises(_native.M3Error):
+            ctx.apply_actions(boards[:1], [1], 20, 0)
+        b = BoardV2(20, BoardConfig(seed=1, rows=R, columns=C, types=T))
+        assert (b.array == g["wide_boards_" + tag][0]).all()
+        with pytest.raises(IndexError):
+            b.legal_actions
+        with pytest.raises(IndexError):
+            b.apply_action(0)
+        env = Match3Env(width=C, height=R, num_types=T, seed=3)
+        with pytest.raises(IndexError):
+            env.step(0)
+        ctx.close()
+
+
+@pytest.mark.parametrize("shape", [(12, 12, 7), (8, 8, 5), (5, 3, 3)], ids=lambda s: "x".join(map(str, s)))
+def test_frame_env_large_batch_vs_oracle(shape):
+    """262,144 boards (C4-sized batch) of a frame shape, 20 seeded moves with autoreset off: size-
+    independent checks on all, every move of a 2,048-board sample against the oracle."""
+    R, C, T = shape
+    n = 1 << 18
+    env = BatchedMatch3Env(n, R, C, T, num_moves=20, env_goal=BIG, seed_base=11, autoreset=False, shards=2)
+    total = np.zeros(n, np.int64)
+    idx = np.random.default_rng(0).choice(n, 2048, replace=False)
+    rews, acts = [], []
+    for _ in range(20):
+        acts.append(env.next_actions()[idx])
+        env.step()
+        r = env.rewards()
+        assert (r >= 0).all()
+        total += r
+        rews.append(r[idx])
+    assert (env.scores() == total).all() and (env.moves() == 20).all()
+    cap = (env.flags() & (_native.FLAG_SHUFFLE_CAP | _native.FLAG_CASCADE_CAP)) != 0
+    o = Oracle(R, C, T, episode_shuffle_cap=1024).batch_episodes((idx + 11).astype(np.uint32), 20, BIG)
+    ok = (o["moves"] == 20) & ~cap[idx]
+    assert ok.mean() > 0.95
+    assert (np.array(acts).T[ok] == o["actions"][ok]).all()
+    assert (np.array(rews).T[ok] == o["rewards"][ok]).all()
+    assert (env.observations().reshape(n, -1)[idx][ok] == o["final"][ok]).all()
+    env.close()
+
+
+def test_frame_rollouts_and_autoreset_vs_oracle():
+    """MCTS rollouts (f3) and same-step autoreset (f1) on a frame shape."""
+    R, C, T = 10, 8, 5
+    ctx = _native.Context(R, C, T)
+    seeds = np.arange(1, 4097, dtype=np.uint32)
+    boards, _, _ = ctx.init_boards(seeds)
+    rs = (np.arange(4096, dtype=np.uint64) * 2654435761 % (2**31)).astype(np.uint32)
+    ro = ctx.rollouts(boards, seeds, 20, rs)
+    want = Oracle(R, C, T).rollouts(boards.astype(np.int32), seeds, 20, rs, threads=4)
+    assert (ro["gain"] == want["gain"]).all() and (ro["steps"] == want["steps"]).all()
+    assert (ro["draws"] == want["draws"]).all()
+    n = 2048
+    env = BatchedMatch3Env(n, R, C, T, num_moves=5, env_goal=BIG, seed_base=100, autoreset=True, seed_stride=n)
+    for _ in range(5):
+        env.step()
+    assert env.dones().all()
+    fresh, _, first = ctx.init_boards(np.arange(100 + n, 100 + 2 * n, dtype=np.uint32))
+    assert (env.observations() == fresh).all() and (env.next_actions() == first).all()
+    env.close()
+    ctx.close()
