@@ -67,6 +67,7 @@ constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 template <class CF>
 struct KS {
     static constexpr int B = 64;
+    static_assert(B == 64, "one-wave workgroups: lds_sync() orders a single wave's LDS accesses");
     static constexpr int GCAP = 4;                  // match groups in LDS (more spill to a global pool)
 #ifndef M3_STEP_WPS
 #define M3_STEP_WPS 4
@@ -243,6 +244,23 @@ inline int m3_prof_read_tu(uint64_t* out, int reset) {
     return PH_N;
 }
 #endif
+
+// Staging barrier of the one-wave (64-lane) workgroups: it only has to order
+// this wave's own LDS accesses (a wave's DS instructions execute in issue
+// order), so a wavefront-scope fence suffices. __syncthreads() would also make
+// the wave wait for every global store it has in flight (vmcnt(0) of the
+// workgroup-scope release), i.e. a full memory round trip per kernel tail.
+#ifndef M3_WAVE_SYNC
+#define M3_WAVE_SYNC 0
+#endif
+__device__ __forceinline__ void lds_sync() {
+#if M3_WAVE_SYNC
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#else
+    __syncthreads();
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // LDS staging
@@ -429,7 +447,7 @@ __global__ void __launch_bounds__(KS<CF>::B) k_apply(ApplyArgs a) {
     const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
     const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
     block_copy_in<KS<CF>::B>(a.boards + b0 * NC, lds, nb * NC);
-    __syncthreads();
+    lds_sync();
     const int t = threadIdx.x;
     if (t < nb) {
         const int64_t b = b0 + t;
@@ -445,7 +463,7 @@ __global__ void __launch_bounds__(KS<CF>::B) k_apply(ApplyArgs a) {
         }
         planes_to_bytes<CF>(P, lds + t * NC, dm);
     }
-    __syncthreads();
+    lds_sync();
     block_copy_out<KS<CF>::B>(a.out_boards + b0 * NC, lds, nb * NC);
 }
 
@@ -857,7 +875,7 @@ __global__ void __launch_bounds__(KS<CF>::B) k_legal(Shape shape, int64_t n, con
     const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
     const int nb = (int)((n - b0) < KS<CF>::B ? (n - b0) : KS<CF>::B);
     block_copy_in<KS<CF>::B>(boards + b0 * NC, lds, nb * NC);
-    __syncthreads();
+    lds_sync();
     const int t = threadIdx.x;
     if (t < nb) {
         typename CF::Bd P[CF::NP], HL, VL;
@@ -1071,7 +1089,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     block_copy_in<KS<CF>::B>(a.cur + b0 * NC, lds, nb * NC);
     const int t = threadIdx.x;
     const uint32_t cslot = t < nb ? a.slot[b0 + t] : 0u;
-    __syncthreads();
+    lds_sync();
 #ifdef M3_PHASE_PROF
     M3_PROF_LDS(KS<CF>::B)
     Prof<LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>> st;
@@ -1133,7 +1151,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
             }
         }
     }
-    __syncthreads();
+    lds_sync();
     block_copy_out<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
 #ifdef M3_PHASE_PROF
     if (live) st.end(0);
@@ -1293,11 +1311,11 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_rollout(Rollout
     const int64_t b0 = (int64_t)blockIdx.x * K::B;
     const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
     block_copy_in<K::B>(a.boards + b0 * NC, lds, nb * NC);
-    __syncthreads();
+    lds_sync();
     const int t = threadIdx.x;
     typename CF::Bd P[CF::NP];
     if (t < nb) lds_to_planes<CF>(lds, t, P, dm);
-    __syncthreads();
+    lds_sync();
     LdsStore<CF, K::GCAP, K::B> st{stage_tab + t};
     st.spill = a.spill;
     st.pool_next = &a.counters[1];
@@ -1314,9 +1332,9 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_rollout(Rollout
         }
     }
     if (!a.out_boards) return;
-    __syncthreads();
+    lds_sync();
     if (t < nb) planes_to_bytes<CF>(P, lds + t * NC, dm);
-    __syncthreads();
+    lds_sync();
     block_copy_out<K::B>(a.out_boards + b0 * NC, lds, nb * NC);
 }
 
@@ -1602,8 +1620,10 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.stats = base + 41;
         prefetch_args<CF>(e, o, r);
         // the grid is sized for the expected number of finished boards and grid-strides
+#ifndef M3_DEBUG_NO_PREFETCH  // timing experiment only: the next episodes are never built (not bit-exact)
         int rc = launch_init<CF>(sh.pstream, r, sh.n / 8 + 1);
         if (rc) return rc;
+#endif
         // the resets were the block's last readers: zero it here, off the step's critical path
         HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), sh.pstream));
         HIP_TRY(hipEventRecord(sh.pev[par], sh.pstream));
