@@ -58,6 +58,7 @@ M3_HD uint32_t mt_state397(uint32_t seed) {
 template <uint32_t LIMIT>
 struct ChainMTT {
     static_assert(LIMIT == 227u || LIMIT == 624u, "chain depth");
+    static constexpr bool DRAW_BOUNDED = true;  // overflow after LIMIT draws (bounds the cascade)
     uint32_t seed, mt397;
     uint32_t k;           // raw outputs since the last reseed
     uint32_t a_lo, a_hi;  // mt[k], mt[k+397]

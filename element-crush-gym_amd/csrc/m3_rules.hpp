@@ -62,6 +62,15 @@ enum : uint32_t {
 // Steps of the supported shapes use 1-10 passes; the cap is a
 // safety bound, flagged when hit (parity undefined there, as at the shuffle cap).
 constexpr int CASCADE_CAP = 1024;
+// An RNG that raises `overflow` after a fixed number of draws (ChainMT: 624)
+// bounds the cascade by itself -- every pass that continues refills >= 3
+// cleared cells -- so the specialised shapes on such a stream skip the pass
+// counter: it would be one more register live through the step kernels'
+// cascade (measured: 5 % / 11 % slower at 9x9x6 / 16x16x8 from the spills).
+template <class R, class = void>
+struct DrawBounded : std::false_type {};
+template <class R>
+struct DrawBounded<R, std::void_t<decltype(R::DRAW_BOUNDED)>> : std::bool_constant<R::DRAW_BOUNDED> {};
 
 template <class CF>
 struct StaticDim;
@@ -1042,9 +1051,11 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
         if (!settled) {
             for (;;) {  // cascade: refill, rematch, clear while matches remain
                 if (it == limit) return CAS_PAUSED;             // paused before iteration limit + 1
-                if (it >= CASCADE_CAP) {
-                    flags |= FLAG_CASCADE_CAP;
-                    break;
+                if constexpr (CF::DYN || !DrawBounded<RNG>::value) {
+                    if (it >= CASCADE_CAP) {
+                        flags |= FLAG_CASCADE_CAP;
+                        break;
+                    }
                 }
                 ++it;
                 const Bd em = gravity<CF>(P, dm);               // :166-173
@@ -1215,8 +1226,9 @@ M3_HD void init_board(typename CF::Bd* P, RNG& mt, S& st, const typename CF::Dim
 // appended to plane words in `tm`, plane p word w at tm[(p*TWMAX + w)*stride]).
 // Raw outputs k < rawn and their acceptance bits go to the sinks (the
 // kernels pass rawn = 0; the host harness uses them to check the stream).
-// Returns false if the board needs more than the first MT block (624 draws):
-// the caller recomputes it. `draws` = raw outputs consumed by __init__.
+// Returns false if the board needs more than the first kcap draws (at most
+// the first MT block, 624): the caller recomputes it. `draws` = raw outputs
+// consumed by __init__.
 // --------------------------------------------------------------------------
 template <class CF>
 struct TileGen {
@@ -1235,7 +1247,8 @@ M3_HD bool wave_any(bool p) {
 
 template <class CF, class RNG, class RawSink, class AccSink, class S = NoStore>
 M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* pos, int stride, uint32_t& draws,
-                            uint32_t rawn, RawSink raw_sink, AccSink acc_sink, S* ps = nullptr) {
+                            uint32_t rawn, RawSink raw_sink, AccSink acc_sink, S* ps = nullptr,
+                            uint32_t kcap = 624u) {
     using Bd = typename CF::Bd;
     using G = typename CF::G;
     constexpr int TW = TileGen<CF>::TWMAX, N = CF::N, MAXR = TileGen<CF>::MAXR;
@@ -1285,8 +1298,8 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
     };
     // make sure every lane that still needs them has `need` tiles (or the block is exhausted)
     auto ensure = [&](uint32_t need, bool want) {
-        while (wave_any(want && nt < need) && g.k < 624u) {
-            const uint32_t kend = g.k + 64u < 624u ? g.k + 64u : 624u;
+        while (wave_any(want && nt < need) && g.k < kcap) {
+            const uint32_t kend = g.k + 64u < kcap ? g.k + 64u : kcap;
             gen_to(kend);
         }
         return !want || nt >= need;

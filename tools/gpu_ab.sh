@@ -2,6 +2,7 @@
 # the spec passes --shape). A variant is timed only after the bit-exactness suite passes
 # against it (tests/test_gpu_parity.py + test_gpu_env.py with M3_LIB pointing at the variant);
 # a variant that fails is reported as REJECTED and never timed.
+# PARITY_TESTS overrides the gating test files (e.g. for a library built before a test existed).
 # usage: bash tools/gpu_ab.sh <tag> "<lib> <bench args>" ...   (lib relative to element-crush-gym_amd/build)
 set -o pipefail
 export TMPDIR=/tmp
@@ -16,7 +17,7 @@ for spec in "$@"; do
   i=$((i+1))
   export M3_LIB=$PWD/element-crush-gym_amd/build/$L
   if [ -z "${GATED[$L]}" ]; then
-    timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_env.py -m gpu -x -q \
+    timeout -k 10 600 python3 -u -m pytest ${PARITY_TESTS:-tests/test_gpu_parity.py tests/test_gpu_env.py} -m gpu -x -q \
       --timeout 300 --timeout-method thread > $OUT/parity_$L.log 2>&1
     rc=$?
     if [ $rc -ge 124 ]; then echo "$L: parity run killed/timed out (rc=$rc)"; exit 1; fi
