@@ -683,39 +683,60 @@ __device__ __forceinline__ void wave_fill(uint32_t* key, uint8_t* cells, int lan
     wave_sync();
 }
 
-// One reset (item of the launch) by the whole wave; key: 624 words of LDS, cells: N bytes of LDS.
+// init_genrand(seed) into key[0..623]. The recurrence is serial and the seed
+// wave-uniform, so it runs on the scalar unit; v_writelane gathers 64
+// consecutive values into one VGPR and a single LDS store writes them.
+__device__ __forceinline__ void wave_init_key(uint32_t* key, uint32_t seed, int lane) {
+    uint32_t x = __builtin_amdgcn_readfirstlane(seed);
+    for (int blk = 0; blk < 9; ++blk) {  // 9 x 64 + 48 = 624
+        uint32_t col = 0u;
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(col) : "s"(x), "n"(j));
+            x = mt_init_next(x, (uint32_t)(blk * 64 + j) + 1u);
+        }
+        key[blk * 64 + lane] = col;
+    }
+    uint32_t col = 0u;
+#pragma unroll
+    for (int j = 0; j < 48; ++j) {
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(col) : "s"(x), "n"(j));
+        x = mt_init_next(x, (uint32_t)(576 + j) + 1u);
+    }
+    if (lane < 48) key[576 + lane] = col;
+}
+
+// One reset (item of the launch) by the whole wave; key: 624 words of LDS,
+// cells: N bytes of LDS. Returns the draws BoardV2.__init__ consumed.
 template <class CF>
-__device__ void wave_reset(const InitArgs& a, int64_t item, uint32_t* key, uint8_t* cells, int lane) {
+__device__ uint32_t wave_reset(const InitArgs& a, int64_t item, uint32_t* key, uint8_t* cells, int lane) {
     int64_t b;
     uint32_t seed, slot;
     init_item(a, item, b, seed, slot);
-    if (lane == 0) {  // init_genrand is a serial recurrence
-        uint32_t x = seed;
-        for (uint32_t p = 0; p < 624u; ++p) {
-            key[p] = x;
-            x = mt_init_next(x, p + 1u);
-        }
-    }
+    wave_init_key(key, seed, lane);
     wave_sync();
     const uint32_t m397 = key[397];
     uint32_t pos = 624u, k = 0u;
-    wave_fill<CF>(key, cells, lane, pos, k, nullptr);                  // boardv2.py:21
     typename CF::Bd P[CF::NP], mask;
+    const int64_t ob = (int64_t)slot * a.sstride + b;
+    constexpr int NW = (CF::N + 3) / 4;
+    wave_fill<CF>(key, cells, lane, pos, k, nullptr);               // boardv2.py:21
     planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
-    while (get_match_mask<CF>(P, mask)) {                               // boardv2.py:23-27
+    while (get_match_mask<CF>(P, mask)) {                           // boardv2.py:23-27
         wave_fill<CF>(key, cells, lane, pos, k, &mask);
         planes_from_words<CF>(reinterpret_cast<const uint32_t*>(cells), P);
     }
-    const int64_t ob = (int64_t)slot * a.sstride + b;
+    if (a.m397 && lane == 0) a.m397[(int64_t)slot * a.cstride + b] = m397;
     if (lane == 0) init_outputs<CF>(a, b, ob, seed, m397, k, P);
     if (a.board_words) {
-        for (int q = lane; q < (CF::N + 3) / 4; q += 64)
-            a.board_words[ob * ((CF::N + 3) / 4) + q] = reinterpret_cast<const uint32_t*>(cells)[q];
+        for (int q = lane; q < NW; q += 64)
+            a.board_words[ob * NW + q] = reinterpret_cast<const uint32_t*>(cells)[q];
     } else {
         int8_t* dst = a.boards + ob * CF::N;
         for (int x = lane; x < CF::N; x += 64) dst[x] = (int8_t)cells[x];
     }
     wave_sync();
+    return k;
 }
 
 // Reset on the register-only MT19937 chain; grid-strided over n (or *list_count).
@@ -1211,12 +1232,25 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.cur + b * dm.cells(), P, dm);
-        FullMT mt;  // scratch (see k_apply_fix)
-        mt.init(a.seeds[b], 0u);
         ArrayStore<CF> st;
         int r;
         uint32_t f;
-        env_step_one<CF, false>(P, a, b, mt, st, -1, r, f, dm);
+        int res = ENV_STEP_RECOMPUTE;
+        if constexpr (std::is_same_v<typename KS<CF>::Chain, ChainMT1>) {
+            // the step ran out of the one-level chain (> 226 draws): the
+            // three-level chain covers the whole first block in registers,
+            // where FullMT would walk 2.5 KB of scratch state at memory
+            // latency on the step's critical path
+            ChainMT cm;
+            cm.init(a.seeds[b], a.m397[(int64_t)a.slot[b] * a.cstride + b]);
+            res = env_step_one<CF, false>(P, a, b, cm, st, -1, r, f, dm);
+            if (res == ENV_STEP_RECOMPUTE) bytes_to_planes<CF>(a.cur + b * dm.cells(), P, dm);
+        }
+        if (res == ENV_STEP_RECOMPUTE) {  // >= 624 draws
+            FullMT mt;  // scratch (see k_apply_fix)
+            mt.init(a.seeds[b], 0u);
+            env_step_one<CF, false>(P, a, b, mt, st, -1, r, f, dm);
+        }
         planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
     }
 }
@@ -1498,10 +1532,11 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     if (max_items == 0) return M3_OK;
     int64_t g = (max_items + INIT_BLOCK - 1) / INIT_BLOCK;
     if (g > 4096) g = 4096;
-    if constexpr (INIT_INLINE_FIX<CF>)
+    if constexpr (INIT_INLINE_FIX<CF>) {
         hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
-    else  // ~60% of 16x16x8 resets overflow the first MT block: FullMT for all
+    } else {  // ~60% of 16x16x8 resets overflow the first MT block: FullMT for all
         hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3((unsigned)g), dim3(INIT_FIX_BLOCK), 0, stream, a);
+    }
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }
