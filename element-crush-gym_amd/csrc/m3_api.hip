@@ -464,6 +464,7 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     alloc(&e->ne_words, (size_t)NSLOT * n * 4ull * ((c->N + 3) / 4));
     alloc(&e->ne_first, (size_t)NSLOT * n * 4);
     alloc(&e->ne_legal, (size_t)NSLOT * n * 4ull * c->AW);
+    alloc(&e->defer, n * 4);
     for (int p = 0; p < PF_LAG; ++p) {
         alloc(&e->pf_list[p], n * 4);
         alloc(&e->pf_seed[p], n * 4);
@@ -545,7 +546,7 @@ int m3_env_destroy(m3_env* e) {
                     e->next_action, e->reward, e->done, e->trunc, e->actions[0], e->actions[1], e->counters,
                     e->ovf_list,
                     e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal,
-                    e->spill, e->m397, e->cont};
+                    e->spill, e->m397, e->cont, e->defer};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < PF_LAG; ++q)

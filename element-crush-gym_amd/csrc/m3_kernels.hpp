@@ -57,6 +57,13 @@ constexpr int INIT_BLOCK = 64;
 template <class CF>
 constexpr bool INIT_INLINE_FIX = CF::N <= 128;
 constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
+// k_init's lockstep draw budget when it may defer (env prefetch): 9x9x6 resets
+// past 454 draws (~4 %: the third chain level and the second block) go to
+// k_init_coop, so a wave no longer runs to its slowest lane's ~600 draws
+#ifndef M3_RESET_KCAP
+#define M3_RESET_KCAP 454
+#endif
+constexpr uint32_t RESET_KCAP = M3_RESET_KCAP;
 
 // Per-shape step-kernel geometry: boards (lanes) per workgroup and the
 // match-group table capacity, sized so staging + table fit the 160 KB LDS.
@@ -522,6 +529,8 @@ struct InitArgs {
     uint32_t* stats;             // nullable: [0] resets, [1] reset recomputes (>= 624 draws)
     uint32_t* m397;              // nullable: mt[397] of the seed's init_genrand state at (slot, b)
     int64_t cstride;
+    uint32_t* defer;             // nullable: items k_init leaves to k_init_coop (reset needs >= RESET_KCAP draws)
+    uint32_t* defer_count;       // device count for defer (zeroed before k_init)
 };
 }  // namespace m3k
 using m3k::InitArgs;
@@ -587,17 +596,17 @@ __device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, int64
 }
 
 // Reset of board b on a tile stream generated in LDS (init_board_tiles).
-// Returns false if the reset needs >= 624 draws (wave_reset / k_init_fix redo it).
+// Returns false if the reset needs >= kcap draws (wave_reset redoes it).
 template <class CF, class S = NoStore>
 __device__ __forceinline__ bool init_emit(const InitArgs& a, int64_t b, uint32_t seed, uint32_t slot, uint32_t m397,
-                                          uint32_t* tm, uint32_t* pos, S* ps = nullptr) {
+                                          uint32_t* tm, uint32_t* pos, S* ps = nullptr, uint32_t kcap = 624u) {
     typename CF::Bd P[CF::NP];
     ChainMT g;
     g.init(seed, m397);
     if (a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;
     uint32_t draws = 0;
     const bool ok = init_board_tiles<CF>(
-        P, g, tm, pos, INIT_BLOCK, draws, 0u, [](uint32_t, uint32_t) {}, [](uint32_t, uint32_t) {}, ps);
+        P, g, tm, pos, INIT_BLOCK, draws, 0u, [](uint32_t, uint32_t) {}, [](uint32_t, uint32_t) {}, ps, kcap);
     if (!ok) return false;
     const int64_t ob = (int64_t)slot * a.sstride + b;
     init_outputs<CF>(a, b, ob, seed, m397, draws, P);
@@ -770,14 +779,25 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
             uint32_t seed, slot;
             init_item(a, i, b, seed, slot);
             const uint32_t m397 = mt_state397(seed);
+            const uint32_t kcap = a.defer ? RESET_KCAP : 624u;
 #ifdef M3_PHASE_PROF
-            ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, &ps);
+            ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, &ps, kcap);
 #else
-            ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, pp);
+            ok = init_emit<CF>(a, b, seed, slot, m397, tm, pos, pp, kcap);
 #endif
         }
-        // this wave redoes its >= 624-draw resets at once
         uint64_t bad = __ballot(!ok);
+        if (a.defer) {  // left to k_init_coop: one wave-aggregated append
+            if (bad) {
+                const int lane = (int)threadIdx.x;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(a.defer_count, (uint32_t)__popcll(bad));
+                base = __shfl(base, 0);
+                if (!ok) a.defer[base + (uint32_t)__popcll(bad & ((1ull << lane) - 1ull))] = (uint32_t)i;
+            }
+            continue;
+        }
+        // this wave redoes its >= 624-draw resets at once
         if (bad && a.stats && threadIdx.x == 0) atomicAdd(&a.stats[1], (uint32_t)__builtin_popcountll(bad));
         while (bad) {
             const int l = __builtin_ctzll(bad);
@@ -788,6 +808,20 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
 #ifdef M3_PHASE_PROF
     if (live) ps.end(1);
 #endif
+}
+
+// The resets k_init deferred (>= RESET_KCAP draws), one wave per board
+// (wave_reset), grid-strided over the device-side count.
+template <class CF>
+__global__ void __launch_bounds__(64) k_init_coop(InitArgs a) {
+    __shared__ uint32_t key_s[624];
+    __shared__ __attribute__((aligned(16))) uint8_t cell_s[(CF::N + 3) / 4 * 4 + 16];
+    const uint32_t cnt = *a.defer_count;
+    const int lane = (int)threadIdx.x;
+    for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
+        const uint32_t k = wave_reset<CF>(a, a.defer[q], key_s, cell_s, lane);
+        if (a.stats && lane == 0 && k >= 624u) atomicAdd(&a.stats[1], 1u);
+    }
 }
 
 // ---- lane-per-board reset for boards that need >= 624 draws -------------
@@ -1455,7 +1489,7 @@ struct m3_env {
     bool upload_pend[2] = {false, false};  // upload_ev[p] recorded and not yet waited on by the host
     bool upload_this = false;              // the step being enqueued reads actions[step & 1]
     // counters, 64 words per shard: [8q + 0] step overflow count, [8q + 1]
-    // prefetch queue length, [8q + 2] prefetch overflow count, [8q + 3] spill
+    // prefetch queue length, [8q + 2] deferred prefetch resets, [8q + 3] spill
     // records taken, [8q + 4] continuation records (q = step % PF_LAG); stats
     // [40] step recomputes, [41] resets, [42] reset recomputes; [48 + k] the
     // reset / slot-fill overflow counts (shard 0's block)
@@ -1470,6 +1504,7 @@ struct m3_env {
     uint32_t* ne_legal = nullptr;
     uint32_t* m397 = nullptr;  // [NSLOT][n]
     uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont)
+    uint32_t* defer = nullptr; // prefetch resets k_init leaves to k_init_coop [n]
     // prefetch queues and their overflow lists, by step % PF_LAG
     uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {};
     int64_t steps = 0;
@@ -1534,6 +1569,12 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     if (g > 4096) g = 4096;
     if constexpr (INIT_INLINE_FIX<CF>) {
         hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
+        if (a.defer) {  // sized for the usual ~4 % deferred share, grid-strided
+            HIP_TRY(hipGetLastError());
+            int64_t gc = max_items / 16 + 1;
+            gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+            hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
+        }
     } else {  // ~60% of 16x16x8 resets overflow the first MT block: FullMT for all
         hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3((unsigned)g), dim3(INIT_FIX_BLOCK), 0, stream, a);
     }
@@ -1653,6 +1694,10 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.list_slot = e->pf_slot[par] + o;
         r.list_count = &cnt[1];
         r.stats = base + 41;
+        if constexpr (INIT_INLINE_FIX<CF>) {
+            r.defer = e->defer + o;
+            r.defer_count = &cnt[2];  // zeroed with the block
+        }
         prefetch_args<CF>(e, o, r);
         // the grid is sized for the expected number of finished boards and grid-strides
 #ifndef M3_DEBUG_NO_PREFETCH  // timing experiment only: the next episodes are never built (not bit-exact)
