@@ -91,16 +91,17 @@ VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2
 
 
 def load_profile(shape_tag, boards, boards_per_launch):
-    """The committed rocprofv3 PMC summary of the step kernel (profiles/traffic.json), if one matches."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)
-        if (t.get("shape") == shape_tag and int(t.get("boards")) == boards
-                and int(t.get("boards_per_launch", -1)) == boards_per_launch):
-            return t
-    except Exception:
-        pass
+    """The committed rocprofv3 PMC summary of the step kernel (profiles/traffic_<shape>.json, or
+    profiles/traffic.json for the headline shape), if one matches this configuration."""
+    for name in (f"traffic_{shape_tag}.json", "traffic.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                t = json.load(f)
+            if (t.get("shape") == shape_tag and int(t.get("boards")) == boards
+                    and int(t.get("boards_per_launch", -1)) == boards_per_launch):
+                return t
+        except Exception:
+            pass
     return {}
 
 
@@ -425,7 +426,8 @@ def main():
             "avg_kernel_ms": avg_kernel_s * 1e3,
             # the shards' launches overlap, so per launch understates the whole GPU's rate
             "aggregate_gbs": value / world * algorithmic_bytes_per_step(rows, cols) / 1e9,
-            "note": "integer-VALU bound path; HBM roofline per BASELINE/SURVEY §8(d): 183 B per 9x9 env-step",
+            "note": f"integer-VALU bound path; HBM roofline per BASELINE/SURVEY §8(d): "
+                    f"{algorithmic_bytes_per_step(rows, cols)} B per {rows}x{cols} env-step (2RC + 21)",
             # the resource that binds: VALU issue (wave64 instructions from the committed PMC pass
             # over the live per-launch time), against the chip's VALU issue peak
             "valu": None if not valu else {

@@ -5,7 +5,8 @@
 
 Writes profiles/<round-tag>_bench.json (the bench line), <round-tag>_kernel_stats.csv
 (rocprofv3 --kernel-trace --stats of the same bench command), <round-tag>_pmc.txt
-(per-kernel PMC means, one rocprofv3 pass per counter group) and traffic.json:
+(per-kernel PMC means, one rocprofv3 pass per counter group) and traffic.json
+(traffic_<shape>.json for a shape other than 9x9x6):
 HBM bytes per launch of one shard's step pipeline (k_env_step + k_env_cont + k_env_fix, the
 two kernels bench.py's HIP events bracket) = 2 * FETCH_SIZE + WRITE_SIZE (KB ->
 bytes), the factor 2 being MI355X_MICROARCH.md's gfx950 correction for wide
@@ -63,5 +64,7 @@ traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"], "kernel": "k_
            "salu_insts_per_launch": per_launch("SQ_INSTS_SALU"),
            "source": f"profiles/{tag}_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
            "correction": "2 x FETCH_SIZE (gfx950 wide-read calibration) + WRITE_SIZE"}
-json.dump(traffic, open(os.path.join(P, "traffic.json"), "w"), indent=1)
+# one summary per board shape: traffic.json (the headline 9x9x6) / traffic_<shape>.json
+tname = "traffic.json" if cfg["shape"] == "9x9x6" else f"traffic_{cfg['shape']}.json"
+json.dump(traffic, open(os.path.join(P, tname), "w"), indent=1)
 print(json.dumps(traffic, indent=1))
