@@ -11,6 +11,11 @@ reward/truncated/done over xGMI. Inputs are resident in HBM before timing.
     python bench.py [--gpus N --steps K --warmup W --boards B]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
+`python bench.py --gpus N` without a launcher starts N rank processes itself
+(one per GPU, LOCAL_RANK = device) from a parent that never touches the GPU;
+under a launcher WORLD_SIZE must equal --gpus. Ranks rendezvous over a plain
+TCP socket (match3tile/rendezvous.py): no torch anywhere in the process.
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -105,45 +110,83 @@ def load_profile(shape_tag, boards, boards_per_launch):
     return {}
 
 
-def dist_setup(world):
-    """Host-side rendezvous of the ranks (torch.distributed over gloo: barriers, the max over ranks,
-    the ncclUniqueId broadcast); RCCL carries the data. None for one process."""
+def dist_setup(rank, world):
+    """Host-side rendezvous of the ranks (barriers, the max over ranks, the ncclUniqueId broadcast)
+    over plain TCP (match3tile/rendezvous.py); RCCL carries the data. None for one process."""
     if world <= 1:
         return None
-    import torch.distributed as dist
+    from match3tile import rendezvous
 
-    dist.init_process_group("gloo")
-    return dist
+    return rendezvous.from_env(rank, world)
+
+
+def dist_close(dist, rank):
+    if dist is None:
+        return
+    dist.barrier()  # every rank done with the server before rank 0 tears it down
+    dist.close()
+    if rank == 0:
+        from match3tile import rendezvous
+
+        rendezvous.cleanup_port_file()
 
 
 def share_unique_id(dist, rank, make_id):
     """Rank 0 makes the 128-byte ncclUniqueId, every rank receives it."""
-    obj = [make_id() if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0)
-    return obj[0]
+    return dist.broadcast(make_id() if rank == 0 else b"", src=0)
 
 
 def gather_check(env, dist, rank, world):
     """After timing: one RCCL all-gather of the last step's packed outcome words, checked against
     every rank's own words (each rank's slice of the gathered buffer must equal what that rank
-    packed locally; compared through a crc exchanged over gloo). True on every rank iff all agree."""
+    packed locally; compared through a crc exchanged over the rendezvous). True on every rank iff
+    all agree."""
     import zlib
 
     import numpy as np
-    import torch
 
     from match3tile.distributed import pack_outcomes
 
     n = env.n
     got = env.gather(to_host=True).reshape(world, n)
     mine = pack_outcomes(env.rewards(), env.truncateds(), env.dones())
-    crcs = [None] * world
-    dist.all_gather_object(crcs, zlib.crc32(mine.tobytes()))
+    crcs = dist.allgather_obj(zlib.crc32(mine.tobytes()))
     ok = bool((got[rank] == mine).all()) and all(zlib.crc32(np.ascontiguousarray(got[r]).tobytes()) == crcs[r]
                                                  for r in range(world))
-    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)
-    return bool(t.item())
+    return all(dist.allgather_obj(ok))
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N rank processes (RANK = LOCAL_RANK = device),
+    host their rendezvous here, and exit with the first failing rank's code (the other ranks are
+    then stopped). This process never touches the GPU (no HIP call before the children start)."""
+    from match3tile.rendezvous import RendezvousServer
+
+    n = args.gpus
+    srv = RendezvousServer(n)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", M3_RDV=srv.address, M3_SPAWNED="1")
+        env.pop("MASTER_PORT", None)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    srv.close()
+    return rc
 
 
 def state_digest(env):
@@ -156,17 +199,19 @@ def state_digest(env):
     return f"{c:08x}"
 
 
-def oracle_sample_check(env, shape, moves, goal, seed_base, stride, total_steps, k=256):
-    """After the clock stops: replay k boards spread over the shard through the C oracle (the
-    checker, never the thing timed) from their first episode, through every same-step autoreset,
-    to the step the env stopped at; compare board, score, moves, seed and the pre-drawn action."""
+def oracle_sample_check(env, shape, moves, goal, seed_base, stride, total_steps, k=256, idx=None):
+    """After the clock stops: replay k boards spread over the shard (or the boards `idx`) through
+    the C oracle (the checker, never the thing timed) from their first episode, through every
+    same-step autoreset, to the step the env stopped at; compare board, score, moves, seed and the
+    pre-drawn action."""
     import numpy as np
 
     from oracle import Oracle
 
     o = Oracle(*shape)
     n = env.n
-    idx = np.unique(np.linspace(0, n - 1, k).astype(np.int64))
+    if idx is None:
+        idx = np.unique(np.linspace(0, n - 1, k).astype(np.int64))
     obs = env.observations().reshape(n, -1)
     score, mv, seeds, nxt = env.scores(), env.moves(), env.seeds(), env.next_actions()
     bad = 0
@@ -195,13 +240,11 @@ def bench_rollouts(a):
     """--rollouts: device MCTS rollouts (m3_rollouts_device), one launch per timed step.
 
     n = --boards states (fresh seeded boards, n_actions = --moves, distinct cfg
-    and rollout seeds) resident in HBM before timing (torch only allocates the
-    device buffers); prints rollouts/s and the env-steps/s inside them, and the
-    C oracle's rate on a bounded host sample (which also checks the gains)."""
-    import ctypes
-
+    and rollout seeds) resident in HBM before timing (device buffers from
+    libm3's own allocator, m3_dev_alloc); prints rollouts/s and the env-steps/s
+    inside them, and the C oracle's rate on a bounded host sample (which also
+    checks the gains)."""
     import numpy as np
-    import torch
 
     from match3tile import _native
 
@@ -214,19 +257,12 @@ def bench_rollouts(a):
     for i in range(0, n, chunk):
         boards[i:i + chunk] = ctx.init_boards(seeds[i:i + chunk])[0].reshape(-1, R * C)
     rseeds = (np.arange(n, dtype=np.uint64) * 2654435761 % (2**31)).astype(np.uint32)
-    dev = torch.device("cuda", 0)
-    d_boards = torch.from_numpy(boards).to(dev)
-    d_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
-    d_na = torch.full((n,), a.moves, dtype=torch.int32, device=dev)
-    d_rs = torch.from_numpy(rseeds.view(np.int32)).to(dev)
-    outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
-    torch.cuda.synchronize()
+    ins = [ctx.device_array(x) for x in (boards, seeds, np.full(n, a.moves, np.int32), rseeds)]
+    outs = [ctx.device_empty(n * 4) for _ in range(4)]
     L = _native.lib()
-    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
     def run():
-        _native.check(L.m3_rollouts_device(ctx.handle, n, p(d_boards), p(d_seeds), p(d_na), p(d_rs),
-                                           *[p(o) for o in outs], None))
+        _native.check(L.m3_rollouts_device(ctx.handle, n, *[d.ptr for d in ins], *[o.ptr for o in outs], None))
 
     for _ in range(max(1, a.warmup)):
         run()
@@ -236,7 +272,8 @@ def bench_rollouts(a):
         run()
     _native.check(L.m3_ctx_synchronize(ctx.handle))
     dt = (time.perf_counter() - t0) / a.steps
-    steps = int(outs[1].sum().item())
+    gain = outs[0].to_host(np.int32, (n,))
+    steps = int(outs[1].to_host(np.int32, (n,)).sum())
     res = {"metric": "MCTS rollouts/s (device, m3_rollouts_device)", "shape": a.shape, "rollouts": n,
            "moves": a.moves, "ms_per_launch": dt * 1e3, "rollouts_per_s": n / dt, "env_steps_per_s": steps / dt,
            "steps_per_rollout": steps / n}
@@ -249,9 +286,12 @@ def bench_rollouts(a):
         t0 = time.perf_counter()
         r = o.rollouts(boards[:m].astype(np.int32), seeds[:m], a.moves, rseeds[:m], threads=threads)
         cdt = time.perf_counter() - t0
-        assert (r["gain"] == outs[0][:m].cpu().numpy()).all(), "device rollouts differ from the oracle"
+        assert (r["gain"] == gain[:m]).all(), "device rollouts differ from the oracle"
         res["cpu_baseline"] = {"rollouts_per_s": m / cdt, "env_steps_per_s": float(r["steps"].sum()) / cdt,
                                "cores": threads, "kind": "port", "sample": f"{m} rollouts, oracle/m3_oracle.c"}
+    for d in ins + outs:
+        d.free()
+    ctx.close()
     print(json.dumps(res))
 
 
@@ -281,6 +321,8 @@ def main():
                          "what each rank received and exit before any GPU work (tests/test_bench_cpu.py)")
     ap.add_argument("--check-boards", type=int, default=256,
                     help="boards per rank replayed through the C oracle after the clock stops (0: none)")
+    ap.add_argument("--allow-stale-lib", action="store_true",
+                    help="if `make` fails, time the library already built (recorded as build.stale in the line)")
     args = ap.parse_args()
     if args.hw_queues is not None:
         if not 1 <= args.hw_queues <= 32:
@@ -288,28 +330,38 @@ def main():
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.rollouts:
         return bench_rollouts(args)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args)  # one process per GPU, this one stays off the GPU
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE); "
+                         f"run `python bench.py --gpus {args.gpus}` (it starts the ranks) or a launcher with "
+                         f"--nproc-per-node {args.gpus}")
     rows, cols, types = (int(x) for x in args.shape.split("x"))
 
-    dist = dist_setup(world)
+    dist = dist_setup(rank, world)
     if args.dry_rendezvous:
         import hashlib
 
         uid = share_unique_id(dist, rank, lambda: os.urandom(128)) if dist else os.urandom(128)
         print(json.dumps({"rank": rank, "world": world, "local_rank": local,
                           "dist_world": dist.get_world_size() if dist else 1,
+                          "spawned": os.environ.get("M3_SPAWNED") == "1", "torch_loaded": "torch" in sys.modules,
                           "id_bytes": len(uid), "id_sha256": hashlib.sha256(uid).hexdigest()}), flush=True)
-        if dist:
-            dist.destroy_process_group()
+        dist_close(dist, rank)
         return
 
     # no-op when libm3.so is up to date with its sources and compile flags (build/flags.stamp);
     # A/B variants are separate files (make variant), selected with M3_LIB (then nothing is
     # built). The ranks of one node share the tree: they take turns under a file lock, so at
-    # most one builds; a failed build falls back to the library already there.
+    # most one builds. A failed build stops the bench unless --allow-stale-lib.
+    build = {"library": os.environ.get("M3_LIB", os.path.join(PKG, "build", "libm3.so")), "make_rc": None,
+             "stale": False}
     if "M3_LIB" not in os.environ:
         import fcntl
 
@@ -318,13 +370,20 @@ def main():
             fcntl.flock(lk, fcntl.LOCK_EX)
             r = subprocess.run(["make", "-s", "-C", PKG])
             fcntl.flock(lk, fcntl.LOCK_UN)
+        build["make_rc"] = r.returncode
         if r.returncode != 0:
-            if not os.path.exists(os.path.join(PKG, "build", "libm3.so")):
-                raise SystemExit("building libm3.so failed and there is no prebuilt library")
-            print("bench.py: make failed; using the existing build/libm3.so", file=sys.stderr)
+            if not (args.allow_stale_lib and os.path.exists(build["library"])):
+                raise SystemExit("bench.py: building libm3.so failed (pass --allow-stale-lib to time the old one)")
+            build["stale"] = True
+            print("bench.py: make failed; timing the existing build/libm3.so (build.stale)", file=sys.stderr)
+    from match3tile import _native
     from match3tile.batched import BatchedMatch3Env
     from match3tile.distributed import seed_plan, timed_steps
 
+    ndev = _native.device_count()
+    if local >= ndev:
+        raise SystemExit(f"bench.py: rank {rank} wants GPU {local} but {ndev} GPU(s) are visible "
+                         f"(--gpus {args.gpus} needs {args.gpus})")
     uid = share_unique_id(dist, rank, BatchedMatch3Env.comm_unique_id) if dist else None
     B = args.boards
     seed_base, seed_stride = seed_plan(rank, world, B)
@@ -348,29 +407,24 @@ def main():
     gather_ok = gather_check(env, dist, rank, world) if dist else None
     parity = {"digest": state_digest(env)}
     if dist:
-        digests = [None] * world
-        dist.all_gather_object(digests, parity["digest"])
-        parity["digest_all_ranks"] = digests
+        parity["digest_all_ranks"] = dist.allgather_obj(parity["digest"])
     if args.check_boards and not args.no_autoreset:
         chk = oracle_sample_check(env, (rows, cols, types), args.moves, args.goal, seed_base, seed_stride,
                                   args.warmup + args.steps, args.check_boards)
         if dist:
-            import torch
-
-            t = torch.tensor([chk["boards"], chk["mismatches"]], dtype=torch.int64)
-            dist.all_reduce(t)
-            chk.update(boards=int(t[0]), mismatches=int(t[1]), ranks=world)
+            nb, nm = dist.allsum([chk["boards"], chk["mismatches"]])
+            chk.update(boards=nb, mismatches=nm, ranks=world)
         parity["oracle_sample"] = chk
         parity["oracle_match"] = chk["mismatches"] == 0
     env.close()
 
     if rank != 0:
-        if dist:
-            dist.destroy_process_group()
+        dist_close(dist, rank)
         return
 
     total_steps = world * B * args.steps
     value = total_steps / elapsed
+    step_s = elapsed / args.steps
     avg_kernel_s = float(kms.mean()) / 1e3 if len(kms) else float("nan")
     # one launch of the step pipeline processes one shard (B / shards boards, contiguous, the last may be short)
     shard_boards = -(-B // stats["shards"])
@@ -378,7 +432,35 @@ def main():
     achieved = bytes_per_launch / avg_kernel_s / 1e9
     prof = load_profile(args.shape, B, shard_boards)
     traffic = prof.get("hbm_bytes_per_launch")
-    valu = prof.get("valu_insts_per_launch")
+    hbm = {
+        # one shard's step pipeline: k_env_step + k_env_cont (the continuation of the
+        # long cascades) + k_env_fix (dead boards, recomputes), bracketed by HIP events
+        # on the shard's stream
+        "kernel": "k_env_step + k_env_cont + k_env_fix",
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic, "algorithmic_bytes_per_launch": bytes_per_launch, "boards_per_launch": shard_boards,
+        "avg_kernel_ms": avg_kernel_s * 1e3,
+        # the shards' launches overlap, so per launch understates the whole GPU's rate
+        "aggregate_gbs": value / world * algorithmic_bytes_per_step(rows, cols) / 1e9,
+        "aggregate_frac": value / world * algorithmic_bytes_per_step(rows, cols) / 1e9 / HBM_PEAK_GBS,
+        "note": f"HBM roofline per BASELINE/SURVEY §8(d): {algorithmic_bytes_per_step(rows, cols)} B per "
+                f"{rows}x{cols} env-step (2RC + 21)"}
+    # The resource that binds is VALU issue: every kernel that runs inside a timed step (the step
+    # pipeline of each shard and the autoreset kernels beside it), wave64 VALU instructions per step
+    # from the committed PMC pass (profiles/traffic*.json, SQ_INSTS_VALU), over the step's wall time,
+    # against the chip's VALU issue peak.
+    vps = prof.get("valu_insts_per_step")
+    if vps:
+        roofline = {
+            "bound": "valu", "kernel": "whole step: " + " + ".join(vps["kernels"]),
+            "achieved": vps["total"] / step_s, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave64 VALU instr/s",
+            "frac": vps["total"] / step_s / VALU_PEAK_WAVE_INSTR_S,
+            "traffic": traffic, "valu_insts_per_step": vps, "ms_per_step": step_s * 1e3,
+            "how": "frac = valu_insts_per_step.total / (ms_per_step / 1e3) / peak; peak = 256 CUs x 4 SIMDs x "
+                   "2.4 GHz / 2 cycles per wave64 VALU instruction",
+            "source": prof.get("source"), "hbm": hbm}
+    else:
+        roofline = dict(hbm, bound="hbm", valu=None)
     out = {
         "metric": METRIC,
         "value": value,
@@ -410,40 +492,14 @@ def main():
         "parity": parity,
         "path_stats": {"autoresets": stats["autoresets"], "reset_recomputes": stats["reset_recomputes"],
                        "step_recomputes": stats["step_recomputes"]},
-        "roofline": {
-            "bound": "hbm",
-            # one shard's step pipeline: k_env_step + k_env_cont (the continuation of the
-            # long cascades) + k_env_fix (dead boards, recomputes), bracketed by HIP events
-            # on the shard's stream
-            "kernel": "k_env_step + k_env_cont + k_env_fix",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": bytes_per_launch,
-            "boards_per_launch": shard_boards,
-            "avg_kernel_ms": avg_kernel_s * 1e3,
-            # the shards' launches overlap, so per launch understates the whole GPU's rate
-            "aggregate_gbs": value / world * algorithmic_bytes_per_step(rows, cols) / 1e9,
-            "note": f"integer-VALU bound path; HBM roofline per BASELINE/SURVEY §8(d): "
-                    f"{algorithmic_bytes_per_step(rows, cols)} B per {rows}x{cols} env-step (2RC + 21)",
-            # the resource that binds: VALU issue (wave64 instructions from the committed PMC pass
-            # over the live per-launch time), against the chip's VALU issue peak
-            "valu": None if not valu else {
-                "achieved": valu / avg_kernel_s, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave64 VALU instr/s",
-                "frac": valu / avg_kernel_s / VALU_PEAK_WAVE_INSTR_S, "insts_per_launch": valu,
-                # all shards' launches of a step over the step's wall time
-                "aggregate_frac": valu * stats["shards"] / (elapsed / args.steps) / VALU_PEAK_WAVE_INSTR_S,
-                "source": prof.get("source")},
-        },
+        "roofline": roofline,
+        "build": build,
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(rows, cols, types, args.moves, args.goal, args.cpu_seconds)
     print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    dist_close(dist, rank)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -209,6 +209,32 @@ int m3_ctx_synchronize(m3_ctx* c) {
     return M3_OK;
 }
 
+int m3_dev_alloc(m3_ctx* c, int64_t bytes, void** out) {
+    CHECK_ARG(c && out && bytes >= 0, "bad arguments");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMalloc(out, bytes ? (size_t)bytes : 4));
+    return M3_OK;
+}
+
+int m3_dev_free(m3_ctx* c, void* p) {
+    CHECK_ARG(c, "null ctx");
+    if (!p) return M3_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));  // the context's work may still use it
+    HIP_TRY(hipFree(p));
+    return M3_OK;
+}
+
+int m3_dev_copy(m3_ctx* c, void* dst, const void* src, int64_t bytes, int kind) {
+    CHECK_ARG(c && dst && src && bytes >= 0 && (kind == 1 || kind == 2), "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return M3_OK;
+}
+
 int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boards, uint32_t* out_draws,
                    int32_t* out_first_action) {
     CHECK_ARG(c && n >= 0 && (n == 0 || (seeds && out_boards)), "bad arguments");
@@ -481,6 +507,14 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     });
     for (hipEvent_t& ev : e->gev)
         if (err == hipSuccess) err = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    // every per-board field starts zeroed: a never-reset env reads back zeros, not stale device memory
+    {
+        void* zp[] = {e->boards[0], e->boards[1], e->seeds, e->flags, e->draws, e->legal, e->score, e->moves,
+                      e->next_action, e->reward, e->done, e->trunc, e->slot};
+        size_t zb[] = {bytes, bytes, n * 4ull, n * 4ull, n * 4ull, n * 4ull * c->AW, n * 4ull, n * 4ull,
+                       n * 4ull, n * 4ull, (size_t)n, (size_t)n, (size_t)n};
+        for (int i = 0; i < 13 && err == hipSuccess; ++i) err = hipMemset(zp[i], 0, zb[i]);
+    }
     if (err != hipSuccess) {
         m3_env_destroy(e);
         return set_err(M3_ERR_HIP, "env allocation (%lld boards): %s", (long long)n, hipGetErrorString(err));
@@ -604,6 +638,7 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     e->ready = true;
+    e->stale = false;
     return M3_OK;
 }
 
@@ -622,7 +657,9 @@ int m3_env_set_autoreset(m3_env* e, int enabled, uint32_t seed_stride) {
 
 int m3_env_step_device(m3_env* e, const int32_t* d_actions) {
     CHECK_ARG(e, "null env");
-    if (!e->ready) return set_err(M3_ERR_STATE, "m3_env_step before m3_env_reset");
+    if (!e->ready)
+        return set_err(M3_ERR_STATE, "m3_env_step before m3_env_reset (or before m3_env_set of boards, seeds, "
+                                     "score, moves and next_action)");
     HIP_TRY(hipSetDevice(e->ctx->device));
     return with_shape(e->ctx->shape, [&](auto cf) {
         if (e->stale) {
@@ -641,8 +678,14 @@ int m3_env_step_device(m3_env* e, const int32_t* d_actions) {
 int m3_env_step(m3_env* e, const int32_t* actions) {
     CHECK_ARG(e, "null env");
     if (!actions) return m3_env_step_device(e, nullptr);
-    if (!e->ready) return set_err(M3_ERR_STATE, "m3_env_step before m3_env_reset");
+    if (!e->ready)
+        return set_err(M3_ERR_STATE, "m3_env_step before m3_env_reset (or before m3_env_set of boards, seeds, "
+                                     "score, moves and next_action)");
     HIP_TRY(hipSetDevice(e->ctx->device));
+    // a loaded env rederives (and restarts the step counter) before the upload buffer's parity is
+    // chosen: the kernel of this step reads actions[steps & 1] of the counter it runs under
+    int rc0 = ensure_fresh(e);
+    if (rc0) return rc0;
     const size_t bytes = (size_t)e->n * 4;
     if (!e->ustream) {
         HIP_TRY(hipStreamCreateWithFlags(&e->ustream, hipStreamNonBlocking));
@@ -731,7 +774,12 @@ int m3_env_set(m3_env* e, int what, const void* host_in) {
     if (rc) return rc;
     HIP_TRY(hipMemcpy(p, host_in, bytes, hipMemcpyHostToDevice));
     e->stale = true;
-    e->ready = true;
+    // stepping needs the whole state: after a reset any field may be overwritten; a fresh env is
+    // ready once boards, seeds, score, moves and the pre-drawn action have all been loaded
+    constexpr uint32_t NEED = (1u << M3_ENV_BOARDS) | (1u << M3_ENV_SEEDS) | (1u << M3_ENV_SCORE) |
+                              (1u << M3_ENV_MOVES) | (1u << M3_ENV_NEXT_ACTION);
+    e->loaded |= 1u << what;
+    if ((e->loaded & NEED) == NEED) e->ready = true;
     return M3_OK;
 }
 

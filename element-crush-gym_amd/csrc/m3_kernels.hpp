@@ -819,8 +819,8 @@ __global__ void __launch_bounds__(64) k_init_coop(InitArgs a) {
     const uint32_t cnt = *a.defer_count;
     const int lane = (int)threadIdx.x;
     for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
-        const uint32_t k = wave_reset<CF>(a, a.defer[q], key_s, cell_s, lane);
-        if (a.stats && lane == 0 && k >= 624u) atomicAdd(&a.stats[1], 1u);
+        wave_reset<CF>(a, a.defer[q], key_s, cell_s, lane);
+        if (a.stats && lane == 0) atomicAdd(&a.stats[1], 1u);
     }
 }
 
@@ -835,6 +835,11 @@ __global__ void __launch_bounds__(64) k_init_coop(InitArgs a) {
 // draws a tile for EVERY cell in row-major order; cells outside `only` take
 // their draw and drop it (array[mask] = new[mask]). A plane word collects 32
 // tiles, then merges under the mask.
+template <class R, class = void>
+struct HasBulk : std::false_type {};
+template <class R>
+struct HasBulk<R, std::void_t<decltype(std::declval<R&>().bulk_ready(1u))>> : std::true_type {};
+
 template <class CF, class RNG>
 __device__ __forceinline__ void fill_round(typename CF::Bd* P, RNG& mt, const typename CF::Bd* only) {
 #pragma unroll
@@ -845,7 +850,7 @@ __device__ __forceinline__ void fill_round(typename CF::Bd* P, RNG& mt, const ty
 #pragma unroll
         for (int p = 0; p < BITS; ++p) t[p] = 0u;
         int bit = 0;
-        if constexpr (CF::TILE_RNG != 0u && CF::TILE_RNG == CF::TILE_MASK) {
+        if constexpr (CF::TILE_RNG != 0u && CF::TILE_RNG == CF::TILE_MASK && HasBulk<RNG>::value) {
             // T a power of two: every draw is a tile, so a word is nbits consecutive outputs
             if (mt.bulk_ready((uint32_t)nbits)) {
 #pragma unroll
@@ -912,6 +917,78 @@ __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
         }
         const uint64_t m = __ballot(long_reset);
         if (m && a.stats && (threadIdx.x & 63) == 0) atomicAdd(&a.stats[1], (uint32_t)__popcll(m));
+    }
+}
+
+// ---- lane-per-board reset on the two-block register chain (16x16x8) -------
+// Every reset of the launch, one board per lane, on ChainMT2: the first 1248
+// raw outputs of seed(s) from registers (m3_rng.hpp), so no reset walks a
+// 2.5 KB lane-private state in scratch. With a power-of-two tile count every
+// round of randint(1, T+1, (R, C)) takes exactly R*C draws (16x16x8: 256), so
+// the lanes of a wave draw in lockstep and the chain's level changes are
+// wave-uniform. A reset that would need a round past draw 1248 (16x16x8: a
+// 5th round, ~2 % of resets) leaves the lane: appended to the defer list for
+// k_init_coop (env prefetch), or redone by its own wave at once (wave_reset)
+// when the launch has no list. stats[1] counts the resets the wave-cooperative
+// pass finishes.
+template <class CF>
+__global__ void __launch_bounds__(INIT_BLOCK) k_init_chain2(InitArgs a) {
+    static_assert(!CF::DYN && INIT_BLOCK == 64, "specialised shapes, one-wave blocks (wave_reset)");
+    constexpr bool LOCKSTEP = CF::TILE_RNG != 0u && CF::TILE_RNG == CF::TILE_MASK;  // N draws per round
+    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
+    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], (uint32_t)cnt);
+    __shared__ uint32_t key_s[624];
+    __shared__ __attribute__((aligned(16))) uint8_t cell_s[(CF::N + 3) / 4 * 4 + 16];
+    const typename CF::Dim dm{};
+    for (int64_t base = (int64_t)blockIdx.x * INIT_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        bool ok = true;
+        if (i < cnt) {
+            int64_t b;
+            uint32_t seed, slot;
+            init_item(a, i, b, seed, slot);
+            const uint32_t m397 = mt_state397(seed);
+            ChainMT2 mt;
+            mt.init(seed, m397);
+            typename CF::Bd P[CF::NP], mask;
+#pragma unroll
+            for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+            fill_round<CF>(P, mt, nullptr);                                     // boardv2.py:21
+            for (;;) {                                                          // :23-27
+                if (mt.overflow) {
+                    ok = false;
+                    break;
+                }
+                if (!get_match_mask<CF>(P, mask)) break;
+                if (LOCKSTEP && mt.k + (uint32_t)CF::N > ChainMT2::LIMIT) {  // the next round leaves the chain
+                    ok = false;
+                    break;
+                }
+                fill_round<CF>(P, mt, &mask);
+            }
+            if (ok) {
+                if (a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;
+                const int64_t ob = (int64_t)slot * a.sstride + b;
+                init_outputs<CF>(a, b, ob, seed, m397, mt.draws(), P, dm);
+                init_store_board<CF>(a, ob, P, dm);
+            }
+        }
+        uint64_t bad = __ballot(!ok);
+        if (!bad) continue;
+        if (a.defer) {  // left to k_init_coop: one wave-aggregated append
+            const int lane = (int)threadIdx.x;
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(a.defer_count, (uint32_t)__popcll(bad));
+            q = __shfl(q, 0);
+            if (!ok) a.defer[q + (uint32_t)__popcll(bad & ((1ull << lane) - 1ull))] = (uint32_t)i;
+            continue;
+        }
+        if (a.stats && threadIdx.x == 0) atomicAdd(&a.stats[1], (uint32_t)__popcll(bad));
+        while (bad) {
+            const int l = __builtin_ctzll(bad);
+            bad &= bad - 1ull;
+            wave_reset<CF>(a, __shfl(i, l), key_s, cell_s, (int)threadIdx.x);
+        }
     }
 }
 
@@ -1472,7 +1549,8 @@ struct m3_env {
     int num_moves = 20, goal = 500;
     int autoreset = 0;
     uint32_t stride = 0;
-    bool ready = false;
+    bool ready = false;  // every state field holds a board's state (m3_env_reset, or m3_env_set of each)
+    uint32_t loaded = 0; // bit `what` per field m3_env_set has loaded since create (ready once all are)
     bool stale = false;  // fields were loaded with m3_env_set: rederive() before the next step
     int8_t* boards[2] = {nullptr, nullptr};
     int cur = 0;
@@ -1575,7 +1653,15 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
             gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
             hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
         }
-    } else {  // ~60% of 16x16x8 resets overflow the first MT block: FullMT for all
+    } else if constexpr (!CF::DYN) {  // 16x16x8: ~60 % of resets need the second MT block
+        hipLaunchKernelGGL(k_init_chain2<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
+        if (a.defer) {  // the ~2 % past draw 1248, one wave per board
+            HIP_TRY(hipGetLastError());
+            int64_t gc = max_items / 32 + 1;
+            gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+            hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
+        }
+    } else {  // frame shapes: FullMT (lane-private scratch)
         hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3((unsigned)g), dim3(INIT_FIX_BLOCK), 0, stream, a);
     }
     HIP_TRY(hipGetLastError());
@@ -1694,7 +1780,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.list_slot = e->pf_slot[par] + o;
         r.list_count = &cnt[1];
         r.stats = base + 41;
-        if constexpr (INIT_INLINE_FIX<CF>) {
+        if constexpr (!CF::DYN) {
             r.defer = e->defer + o;
             r.defer_count = &cnt[2];  // zeroed with the block
         }

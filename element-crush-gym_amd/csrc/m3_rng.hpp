@@ -139,6 +139,162 @@ struct ChainMTT {
 using ChainMT = ChainMTT<624u>;
 using ChainMT1 = ChainMTT<227u>;
 
+// --------------------------------------------------------------------------
+// ChainMT2: the first TWO MT19937 blocks (raw outputs k < 1248) from registers.
+// Resets of 16x16x8 boards draw 256 tiles a round and most need 3-4 rounds
+// (768-1024 draws), past the first block that ChainMT covers.
+//
+// The second twist is mt''[m] = Y ^ twist(mt'[m], mt'[m+1]) with Y =
+// mt'[m+397] (m < 227) or mt''[m-227] (m >= 227), and mt''[623] uses mt''[0]
+// in place of mt'[624]. Every mt' value is again a chain walk (MtpChain, the
+// level structure of ChainMT), so block 2 runs the recursion
+//     L1(m)  = Y1 ^ twist(A1 at m, A1 at m+1),  Y1 = B at 397+m  | L2(m-227)
+//     L2(m') = Y2 ^ twist(A2 at m', ...),        Y2 = B at 397+m' | L3(m'-227)
+//     L3(m") = B at 397+m" ^ twist(A3 at m", ...)
+// with three "A" walks over mt'[0..] (started as block 2, L2 and L3 begin)
+// and ONE "B" walk over mt'[397..623], restarted at each level change (its
+// previous use ends exactly there). B starts mid-sequence, so it needs the
+// init_genrand words s[170] and s[567] besides s[397] (computed once, when a
+// reset first reaches block 2). ~27 registers, no memory; draw 1248 raises
+// `overflow` (the caller hands the board to the wave-cooperative reset).
+// --------------------------------------------------------------------------
+// mt'[i] for consecutive i, over index range [.., LV * 227) (LV = chain levels)
+template <int LV>
+struct MtpChain {
+    uint32_t a_lo, a_hi, b_lo, b_hi, c_lo, c_hi;  // fields of unused levels are never touched
+    M3_HD void start0(uint32_t seed, uint32_t s397) {
+        a_lo = seed;
+        a_hi = s397;
+    }
+    M3_HD void start397(uint32_t s397, uint32_t s170, uint32_t s567) {  // position at i = 397 (LV 3)
+        a_lo = s397;
+        b_lo = s170;
+        b_hi = s567;
+    }
+    // returns mt'[i] and advances to i + 1 (i < 624; i == 623 wraps to mt'[0] as ChainMT)
+    M3_HD uint32_t step(uint32_t i, uint32_t seed, uint32_t s397) {
+        if (LV == 1 || i < 227u) {
+            const uint32_t lo1 = mt_init_next(a_lo, i + 1u);
+            const uint32_t v = a_hi ^ mt_twist(a_lo, lo1);
+            a_hi = mt_init_next(a_hi, i + 398u);
+            a_lo = lo1;
+            return v;
+        }
+        uint32_t lo1a;
+        if (LV >= 3 && i == 623u) lo1a = s397 ^ mt_twist(seed, mt_init_next(seed, 1u));
+        else lo1a = mt_init_next(a_lo, i + 1u);
+        const uint32_t twa = mt_twist(a_lo, lo1a);
+        a_lo = lo1a;
+        const uint32_t j = i - 227u;
+        if (j == 0u) {
+            b_lo = seed;
+            b_hi = s397;
+        }
+        const uint32_t lo1b = mt_init_next(b_lo, j + 1u);
+        const uint32_t twb = mt_twist(b_lo, lo1b);
+        b_lo = lo1b;
+        uint32_t vb;
+        if (LV == 2 || j < 227u) {
+            vb = b_hi ^ twb;
+            b_hi = mt_init_next(b_hi, j + 398u);
+        } else {
+            const uint32_t jj = j - 227u;
+            if (jj == 0u) {
+                c_lo = seed;
+                c_hi = s397;
+            }
+            const uint32_t lo1c = mt_init_next(c_lo, jj + 1u);
+            const uint32_t vc = c_hi ^ mt_twist(c_lo, lo1c);
+            c_hi = mt_init_next(c_hi, jj + 398u);
+            c_lo = lo1c;
+            vb = vc ^ twb;
+        }
+        return vb ^ twa;
+    }
+};
+
+struct ChainMT2 {
+    static constexpr bool DRAW_BOUNDED = true;  // overflow after 1248 draws
+    static constexpr uint32_t LIMIT = 1248u;
+    uint32_t seed, mt397, s170, s567;
+    uint32_t k;
+    uint32_t overflow;
+    MtpChain<3> A1, B;
+    MtpChain<2> A2;
+    MtpChain<1> A3;
+    uint32_t p1, p2, p3, q0;  // previous A1 / A2 / A3 value; mt''[0]
+
+    M3_HD void init(uint32_t s, uint32_t s397) {
+        seed = s;
+        mt397 = s397;
+        overflow = 0u;
+        reseed();
+    }
+    M3_HD void reseed() {
+        k = 0u;
+        A1.start0(seed, mt397);
+    }
+    M3_HD uint32_t draws() const { return k; }
+    M3_HD uint32_t next32() {
+        const uint32_t i = k;
+        uint32_t v;
+        if (i < 624u) {
+            v = A1.step(i, seed, mt397);
+        } else if (i < LIMIT) {
+            v = block2(i - 624u);
+        } else {
+            overflow = 1u;
+            v = 0u;
+        }
+        k = i + 1u;
+        return mt_temper(v);
+    }
+
+  private:
+    M3_HD uint32_t lvl3(uint32_t m) {  // mt''[m], m < 170 (inside L2)
+        if (m == 0u) {
+            A3.start0(seed, mt397);
+            p3 = A3.step(0u, seed, mt397);
+            B.start397(mt397, s170, s567);
+        }
+        const uint32_t c = A3.step(m + 1u, seed, mt397);
+        const uint32_t v = B.step(397u + m, seed, mt397) ^ mt_twist(p3, c);
+        p3 = c;
+        return v;
+    }
+    M3_HD uint32_t lvl2(uint32_t m) {  // mt''[m], m < 397 (inside L1)
+        if (m == 0u) {
+            A2.start0(seed, mt397);
+            p2 = A2.step(0u, seed, mt397);
+            B.start397(mt397, s170, s567);
+        }
+        const uint32_t c = A2.step(m + 1u, seed, mt397);
+        const uint32_t y = m < 227u ? B.step(397u + m, seed, mt397) : lvl3(m - 227u);
+        const uint32_t v = y ^ mt_twist(p2, c);
+        p2 = c;
+        return v;
+    }
+    M3_HD uint32_t block2(uint32_t m) {  // mt''[m], m < 624
+        if (m == 0u) {
+            uint32_t x = seed;
+            for (uint32_t i = 1; i <= 170u; ++i) x = mt_init_next(x, i);
+            s170 = x;
+            x = mt397;
+            for (uint32_t i = 398; i <= 567u; ++i) x = mt_init_next(x, i);
+            s567 = x;
+            A1.start0(seed, mt397);
+            p1 = A1.step(0u, seed, mt397);
+            B.start397(mt397, s170, s567);
+        }
+        const uint32_t c = m < 623u ? A1.step(m + 1u, seed, mt397) : q0;
+        const uint32_t y = m < 227u ? B.step(397u + m, seed, mt397) : lvl2(m - 227u);
+        const uint32_t v = y ^ mt_twist(p1, c);
+        p1 = c;
+        if (m == 0u) q0 = v;
+        return v;
+    }
+};
+
 // Textbook MT19937 (numpy mt19937_seed / mt19937_gen / mt19937_next32).
 // Key is the state's storage: KeyArray = lane-private scratch (an LDS column
 // per lane, one wave per CU, measured slower in k_init_fix_lane). The twist

@@ -32,7 +32,7 @@ ENV_BOARDS, ENV_REWARD, ENV_DONE, ENV_TRUNCATED, ENV_SCORE, ENV_MOVES, ENV_FLAGS
 # every symbol declared in include/m3.h
 EXPORTS = [
     "m3_abi_version", "m3_last_error", "m3_device_count", "m3_supported", "m3_action_space",
-    "m3_ctx_create", "m3_ctx_destroy", "m3_ctx_synchronize",
+    "m3_ctx_create", "m3_ctx_destroy", "m3_ctx_synchronize", "m3_dev_alloc", "m3_dev_free", "m3_dev_copy",
     "m3_init_boards", "m3_apply_actions", "m3_legal_actions", "m3_rollouts", "m3_rollouts_device",
     "m3_env_create", "m3_env_destroy", "m3_env_reset", "m3_env_set_shards", "m3_env_synchronize",
     "m3_env_set_autoreset", "m3_env_step",
@@ -75,6 +75,9 @@ def lib():
             "m3_ctx_create": ([i32, i32, i32, i32, vp], i32),
             "m3_ctx_destroy": ([vp], i32),
             "m3_ctx_synchronize": ([vp], i32),
+            "m3_dev_alloc": ([vp, i64, vp], i32),
+            "m3_dev_free": ([vp, vp], i32),
+            "m3_dev_copy": ([vp, vp, vp, i64, i32], i32),
             "m3_init_boards": ([vp, i64, vp, vp, vp, vp], i32),
             "m3_apply_actions": ([vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
             "m3_legal_actions": ([vp, i64, vp, vp], i32),
@@ -128,6 +131,39 @@ def supported(rows, columns, types) -> bool:
     return bool(lib().m3_supported(rows, columns, types))
 
 
+class DeviceArray:
+    """Device memory on a context's device (m3_dev_alloc): for benches and tests that feed the
+    *_device entry points without a second HIP runtime (torch) in the process."""
+
+    def __init__(self, ctx, nbytes: int):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib().m3_dev_alloc(ctx.handle, self.nbytes, ctypes.byref(p)))
+        self.ptr = p
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a)
+        if a.nbytes != self.nbytes:
+            raise ValueError(f"{a.nbytes} bytes into a {self.nbytes}-byte device array")
+        check(lib().m3_dev_copy(self.ctx.handle, self.ptr, ptr(a), self.nbytes, 1))
+        return self
+
+    def to_host(self, dtype, shape):
+        out = np.empty(shape, dtype)
+        if out.nbytes != self.nbytes:
+            raise ValueError(f"{self.nbytes}-byte device array as {out.nbytes} bytes")
+        check(lib().m3_dev_copy(self.ctx.handle, ptr(out), self.ptr, self.nbytes, 2))
+        return out
+
+    def at(self, offset: int):
+        return ctypes.c_void_p(self.ptr.value + int(offset))
+
+    def free(self):
+        if self.ptr:
+            check(lib().m3_dev_free(self.ctx.handle, self.ptr))
+            self.ptr = None
+
+
 class Context:
     """One HIP stream + scratch on one device for one board shape (m3_ctx)."""
 
@@ -151,6 +187,13 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def device_empty(self, nbytes: int) -> DeviceArray:
+        return DeviceArray(self, nbytes)
+
+    def device_array(self, a) -> DeviceArray:
+        a = np.ascontiguousarray(a)
+        return DeviceArray(self, a.nbytes).upload(a)
 
     # ---- stateless batch calls --------------------------------------------------
     def _boards(self, boards):

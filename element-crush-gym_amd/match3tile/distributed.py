@@ -15,8 +15,9 @@ all-gather of each step's packed outcome words over xGMI (m3_env_gather, include
 * ``timed_steps`` is the bench contract's timed region: W untimed steps, a
   barrier + device sync on both sides of exactly K steps, the max over ranks.
 
-``dist`` arguments are ``torch.distributed`` (any backend: gloo on CPU for
-rendezvous and timing, RCCL carries the data on GPUs) or None for one process.
+``dist`` arguments are a ``match3tile.rendezvous.Rendezvous`` (what bench.py
+uses: plain TCP, no torch), ``torch.distributed`` (the CPU tests' gloo
+groups), or None for one process; RCCL carries the data on GPUs.
 """
 from __future__ import annotations
 
@@ -49,9 +50,19 @@ def unpack_outcomes(packed):
     return p >> 2, ((p >> 1) & 1).astype(bool), (p & 1).astype(bool)
 
 
+def _active(dist) -> bool:
+    if dist is None:
+        return False
+    if hasattr(dist, "allmax"):  # Rendezvous
+        return dist.get_world_size() > 1
+    return dist.is_initialized() and dist.get_world_size() > 1
+
+
 def max_over_ranks(value: float, dist=None) -> float:
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _active(dist):
         return float(value)
+    if hasattr(dist, "allmax"):
+        return dist.allmax(value)
     import torch
 
     t = torch.tensor([float(value)], dtype=torch.float64)
@@ -67,7 +78,7 @@ def timed_steps(step, sync, steps: int, warmup: int, dist=None, on_start=None) -
     for _ in range(warmup):
         step()
     sync()
-    if dist is not None and dist.is_initialized():
+    if _active(dist):
         dist.barrier()
     if on_start is not None:
         on_start()
@@ -76,6 +87,6 @@ def timed_steps(step, sync, steps: int, warmup: int, dist=None, on_start=None) -
         step()
     sync()
     elapsed = time.perf_counter() - t0
-    if dist is not None and dist.is_initialized():
+    if _active(dist):
         dist.barrier()
     return max_over_ranks(elapsed, dist)

@@ -67,6 +67,13 @@ int m3_ctx_create(int device, int rows, int columns, int types, m3_ctx **out);
 int m3_ctx_destroy(m3_ctx *ctx);
 int m3_ctx_synchronize(m3_ctx *ctx);
 
+/* Device memory on the context's device, through the HIP runtime libm3 itself
+ * runs on (host tools and benches need no second runtime, e.g. torch, in the
+ * process). m3_dev_copy blocks; kind 1 = host to device, 2 = device to host. */
+int m3_dev_alloc(m3_ctx *ctx, int64_t bytes, void **out);
+int m3_dev_free(m3_ctx *ctx, void *ptr);
+int m3_dev_copy(m3_ctx *ctx, void *dst, const void *src, int64_t bytes, int kind);
+
 /* ---- stateless batch calls on host buffers (BoardV2 facade) ------------- */
 
 /* BoardV2(n_actions, cfg) with array=None: seeded initial board (boardv2.py:17-27).

@@ -378,6 +378,13 @@ long hc_paused(int reset) {
     if (reset) g_paused = 0;
     return v;
 }
+// first n raw outputs via ChainMT2 (the two-block register chain); -1 once it overflowed
+int hc_chain2_raw(uint32_t seed, int n, uint32_t* out) {
+    ChainMT2 g;
+    g.init(seed, mt_state397(seed));
+    for (int i = 0; i < n; ++i) out[i] = g.next32();
+    return g.overflow ? -1 : 0;
+}
 uint32_t hc_chain_draw(uint32_t seed, int k) {  // k-th raw output (0-based) via ChainMT
     ChainMT g;
     g.init(seed, mt_state397(seed));

@@ -1,8 +1,10 @@
-"""bench.py's N>1 branch on CPU: launched exactly as the driver launches it
-(python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 ...),
-two gloo ranks run the rendezvous and the ncclUniqueId broadcast (a stand-in id: ncclGetUniqueId
-needs a GPU) and stop before any device work. Every rank must be in a world of 2 and hold the
-bytes rank 0 made."""
+"""bench.py's N>1 branch on CPU, in both ways the driver may start it:
+  * `python bench.py --gpus 2` (no launcher): bench.py starts the two rank processes itself;
+  * `python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 ...`.
+Two ranks run the TCP rendezvous (match3tile/rendezvous.py, no torch) and the ncclUniqueId
+broadcast (a stand-in id: ncclGetUniqueId needs a GPU) and stop before any device work. Every
+rank must be in a world of 2 and hold the bytes rank 0 made; a launcher whose world differs from
+--gpus is refused before any device work."""
 import json
 import os
 import socket
@@ -30,6 +32,68 @@ def test_bench_two_rank_rendezvous_and_unique_id_broadcast():
     assert all(x["world"] == 2 and x["dist_world"] == 2 and x["id_bytes"] == 128 for x in lines)
     assert len({x["id_sha256"] for x in lines}) == 1
     assert sorted(x["local_rank"] for x in lines) == [0, 1]
+    assert not any(x["torch_loaded"] for x in lines)
+
+
+def test_bench_spawns_its_ranks_without_a_launcher():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-rendezvous"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert sorted(x["rank"] for x in lines) == [0, 1]
+    assert all(x["world"] == 2 and x["dist_world"] == 2 and x["spawned"] for x in lines)
+    assert len({x["id_sha256"] for x in lines}) == 1 and all(x["id_bytes"] == 128 for x in lines)
+    assert not any(x["torch_loaded"] for x in lines)  # the measurement path never imports torch
+
+
+def test_bench_refuses_a_world_that_differs_from_gpus():
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-rendezvous"],
+                         capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert out.returncode != 0 and "--gpus 2" in out.stderr
+    assert not out.stdout.strip()
+
+
+def test_spawned_rank_failure_stops_the_job():
+    """A rank that fails (here: rank 1 of --gpus 2 on a machine with no GPU) ends the whole job with
+    a non-zero status instead of leaving rank 0 waiting at the rendezvous."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["M3_LIB"] = "/nonexistent/libm3.so"  # no build attempt; every rank fails on the library
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                          "--warmup", "0", "--no-cpu-baseline"], capture_output=True, text=True, timeout=120,
+                         env=env, cwd=ROOT)
+    assert out.returncode != 0
+    assert not [x for x in out.stdout.splitlines() if x.startswith("{")]
+
+
+def test_rendezvous_ops():
+    import threading
+
+    sys.path.insert(0, os.path.join(ROOT, "element-crush-gym_amd"))
+    from match3tile.rendezvous import Rendezvous, RendezvousServer
+
+    srv = RendezvousServer(3)
+    res = [None] * 3
+
+    def rank(r):
+        c = Rendezvous(r, 3, srv.address)
+        got = (c.allgather(bytes([r]) * (r + 1)), c.broadcast(b"id%d" % r, src=0), c.allmax(r * 1.5),
+               c.allsum([r, 1]), c.allgather_obj({"r": r}))
+        c.barrier()
+        c.close()
+        res[r] = got
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(30)
+    for r in range(3):
+        ag, bc, mx, sm, ob = res[r]
+        assert ag == [b"\x00", b"\x01\x01", b"\x02\x02\x02"]
+        assert bc == b"id0" and mx == 3.0 and sm == [3, 3] and ob == [{"r": 0}, {"r": 1}, {"r": 2}]
+    srv.close()
 
 
 def test_host_cores_reports_a_usable_count():

@@ -94,3 +94,50 @@ def test_loaded_boards_step_like_the_stateless_kernel():
     assert (env.next_actions() == ref["next_action"]).all()
     env.close()
     ctx.close()
+
+
+def test_reload_after_odd_step_count_then_host_actions():
+    """A stepped env (odd step count) reloaded and then stepped twice with host actions equals
+    the uninterrupted env: the reload restarts the step counter before the upload buffer of the
+    next host-action step is chosen."""
+    n = 4096
+    a = BatchedMatch3Env(n, 9, 9, 6, num_moves=20, env_goal=400, seed_base=11, autoreset=True, shards=2)
+    for _ in range(3):
+        a.step()
+    st = a.state_dict()
+    b = BatchedMatch3Env(n, 9, 9, 6, num_moves=20, env_goal=400, seed_base=99, autoreset=True, shards=2)
+    for _ in range(7):  # odd: the next host-action upload would pick buffer 1 without the restart
+        b.step()
+    b.load_state_dict(st)  # no read of b before it steps again
+    rng = np.random.default_rng(5)
+    for t in range(4):
+        acts = rng.integers(0, a.A, size=n).astype(np.int32)
+        a.step(acts)
+        b.step(acts)
+    for x, y in zip(_state(a), _state(b)):
+        assert (x == y).all()
+    a.close()
+    b.close()
+
+
+def test_partial_load_is_not_ready_and_fresh_env_reads_zeros():
+    n = 512
+    env = BatchedMatch3Env(n, seeds=False, autoreset=False)
+    st = env.state_dict()  # never reset: zero-initialised fields, not stale device memory
+    for k in ("boards", "seeds", "score", "moves", "next_action", "reward", "flags"):
+        assert not st[k].any(), k
+    ctx = _native.Context(9, 9, 6)
+    boards, _, first = ctx.init_boards(np.arange(1, n + 1, dtype=np.uint32))
+    _native.check(_native.lib().m3_env_set(env.handle, _native.ENV_BOARDS, _native.ptr(boards)))
+    with pytest.raises(_native.M3Error) as e:  # seeds / score / moves / next_action never loaded
+        env.step()
+    assert e.value.code == -6
+    for what, arr in ((_native.ENV_SEEDS, np.arange(1, n + 1, dtype=np.uint32)),
+                      (_native.ENV_SCORE, np.zeros(n, np.int32)), (_native.ENV_MOVES, np.zeros(n, np.int32)),
+                      (_native.ENV_NEXT_ACTION, first)):
+        _native.check(_native.lib().m3_env_set(env.handle, what, _native.ptr(arr)))
+    env.step()  # now complete
+    ref = ctx.apply_actions(boards, np.arange(1, n + 1, dtype=np.uint32), 20, first)
+    assert (env.observations() == ref["boards"]).all()
+    env.close()
+    ctx.close()

@@ -245,3 +245,52 @@ def test_explicit_actions_match_stateless_apply():
         assert (env.observations() == ref["boards"]).all()
         assert (env.rewards() == ref["reward"]).all()
     env.close()
+
+
+def test_c4_262144_boards_autoreset_properties():
+    """Config C4 at its stated size: 262,144 x 16x16x8 boards, 20 steps of seeded random play with
+    same-step autoreset (env_goal 500, so truncated episodes restart mid-run). Every board, every
+    step: values in {1..8, 16, 32} (clip(0, 32), boardv2.py:163: bombs 48 and megas 64 become 32),
+    rewards >= 0, score == sum of the episode's rewards, done == truncated or 20 moves, truncated ==
+    score >= goal; the env's legal bitset == the stateless legal kernel on a sample; then 4,096
+    sampled boards plus every board that shuffled or needed more than the one-level chain's draws
+    (the k_env_fix recompute) replayed through the oracle from their first episode."""
+    import sys
+
+    from conftest import ROOT
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    n, goal = 1 << 18, 500
+    env = BatchedMatch3Env(n, 16, 16, 8, num_moves=20, env_goal=goal, seed_base=1, autoreset=True, shards=2)
+    allowed = np.array(list(range(1, 9)) + [16, 32], np.int8)
+    ep_total = np.zeros(n, np.int64)
+    moves = np.zeros(n, np.int64)
+    special = np.zeros(n, bool)
+    resets = 0
+    for t in range(20):
+        env.step()
+        r, dn, tr = env.rewards(), env.dones(), env.truncateds()
+        assert (r >= 0).all()
+        ep_total += r
+        moves += 1
+        assert (dn == (tr | (moves == 20))).all(), t
+        assert (tr == (ep_total >= goal)).all(), t
+        sc, mv = env.scores(), env.moves()
+        assert (sc[~dn] == ep_total[~dn]).all() and (mv[~dn] == moves[~dn]).all(), t
+        assert (sc[dn] == 0).all() and (mv[dn] == 0).all(), t
+        ep_total[dn] = 0
+        moves[dn] = 0
+        resets += int(dn.sum())
+        special |= ((env.flags() & _native.FLAG_SHUFFLED) != 0) | (env.draws() >= 227)
+        if t in (0, 9, 19):
+            assert np.isin(env.observations(), allowed).all(), t
+    assert resets > n // 4, resets  # truncations restarted episodes mid-run
+    obs = env.observations().reshape(n, -1)
+    idx = np.random.default_rng(1).choice(n, 4096, replace=False)
+    assert (env.ctx.legal_bits(obs[idx]) == env.legal_bits()[idx]).all()
+    idx = np.union1d(idx, np.flatnonzero(special))
+    chk = bench.oracle_sample_check(env, (16, 16, 8), 20, goal, 1, n, 20, idx=idx)
+    assert chk["boards"] == len(idx) and chk["mismatches"] == 0, chk
+    env.close()
