@@ -69,6 +69,83 @@ size_t carve_size(std::initializer_list<size_t> sizes) {
     return s + 256;
 }
 
+// Host-buffer calls stage through one pinned image per direction: the caller's
+// inputs are packed into the context's pinned buffer and go up in ONE copy
+// (which also zeroes the launch's counters, part of the image), the outputs
+// come back in ONE copy and are unpacked -- for the BoardV2 facade's batch-1
+// calls that is two copies, the launches and a sync, instead of a pageable
+// copy per array.
+struct Image {
+    static constexpr int MAXP = 12;
+    size_t off[MAXP] = {}, size[MAXP] = {};
+    int n = 0;
+    size_t total = 0;
+    int add(size_t bytes) {
+        total = (total + 255) & ~size_t(255);
+        off[n] = total;
+        size[n] = bytes;
+        total += bytes;
+        return n++;
+    }
+};
+
+int ensure_host(m3_ctx* c, size_t bytes) {
+    if (c->hcap >= bytes) return M3_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->hbuf) HIP_TRY(hipHostFree(c->hbuf));
+    c->hbuf = nullptr;
+    c->hcap = 0;
+    HIP_TRY(hipHostMalloc(&c->hbuf, bytes, hipHostMallocDefault));
+    c->hcap = bytes;
+    return M3_OK;
+}
+
+// Device scratch = [input image | output image | device-only tail]; the pinned
+// buffer holds the larger of the two images. Returns the device base.
+int stage_begin(m3_ctx* c, const Image& in, const Image& out, size_t tail, char** dev) {
+    const size_t in_sz = (in.total + 255) & ~size_t(255), out_sz = (out.total + 255) & ~size_t(255);
+    int rc = ensure_scratch(c, in_sz + out_sz + tail + 256);
+    if (rc) return rc;
+    rc = ensure_host(c, std::max(in_sz, out_sz) + 256);
+    if (rc) return rc;
+    *dev = (char*)c->dbuf;
+    return M3_OK;
+}
+
+// pack host inputs and upload the image; the same copy zeroes the first
+// `zero_out` bytes of the output image that follows it (the launch's counters)
+int stage_upload(m3_ctx* c, const Image& in, std::initializer_list<const void*> srcs, char* dev,
+                 size_t zero_out = 0) {
+    char* h = (char*)c->hbuf;
+    int i = 0;
+    for (const void* p : srcs) {
+        memcpy(h + in.off[i], p, in.size[i]);
+        ++i;
+    }
+    const size_t in_sz = (in.total + 255) & ~size_t(255);
+    memset(h + in.total, 0, in_sz + zero_out - in.total);
+    HIP_TRY(hipMemcpyAsync(dev, h, in_sz + zero_out, hipMemcpyHostToDevice, c->stream));
+    return M3_OK;
+}
+
+// download the output image, wait, unpack into the caller's buffers (nullptr = skip)
+int stage_download(m3_ctx* c, const Image& out, std::initializer_list<void*> dsts, const char* dev) {
+    char* h = (char*)c->hbuf;
+    HIP_TRY(hipMemcpyAsync(h, dev, out.total, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int i = 0;
+    for (void* p : dsts) {
+        if (p) memcpy(p, h + out.off[i], out.size[i]);
+        ++i;
+    }
+    return M3_OK;
+}
+
+int bad_cells_error(uint32_t waves) {
+    return set_err(M3_ERR_INVALID, "cell value outside [0, 127] in %u wave(s) of 64 boards (outputs undefined)",
+                   waves);
+}
+
 
 
 
@@ -161,7 +238,7 @@ int m3_ctx_create(int device, int rows, int columns, int types, m3_ctx** out) {
     if (sid < 0)
         return set_err(M3_ERR_UNSUPPORTED,
                        "BoardConfig(rows=%d, columns=%d, types=%d): supported are rows and columns 3..16, "
-                       "types 3..15", rows, columns, types);
+                       "types 2..15", rows, columns, types);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return set_err(M3_ERR_NO_DEVICE, "no HIP device visible (libm3 has no CPU fallback)");
@@ -196,6 +273,7 @@ int m3_ctx_destroy(m3_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->dbuf) (void)hipFree(c->dbuf);
+    if (c->hbuf) (void)hipHostFree(c->hbuf);
     if (c->counters) (void)hipFree(c->counters);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -240,30 +318,25 @@ int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boar
     CHECK_ARG(c && n >= 0 && (n == 0 || (seeds && out_boards)), "bad arguments");
     if (n == 0) return M3_OK;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t need = carve_size({n * 4ull, n * (size_t)c->N, n * 4ull, n * 4ull, n * 4ull});
-    int rc = ensure_scratch(c, need);
+    Image in, out;
+    in.add(n * 4ull);
+    const int o_b = out.add(n * (size_t)c->N), o_d = out.add(n * 4ull), o_f = out.add(n * 4ull);
+    char* dev;
+    int rc = stage_begin(c, in, out, 0, &dev);
     if (rc) return rc;
-    Carve cv{(char*)c->dbuf};
-    uint32_t* d_seeds = cv.take<uint32_t>(n);
-    int8_t* d_boards = cv.take<int8_t>(n * c->N);
-    uint32_t* d_draws = cv.take<uint32_t>(n);
-    int32_t* d_first = cv.take<int32_t>(n);
-    HIP_TRY(hipMemcpyAsync(d_seeds, seeds, n * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(c->counters, 0, 16, c->stream));
+    char* dout = dev + ((in.total + 255) & ~size_t(255));
+    rc = stage_upload(c, in, {seeds}, dev);
+    if (rc) return rc;
     InitArgs a{};
     a.shape = c->sdesc;
     a.n = n;
-    a.seeds = d_seeds;
-    a.boards = d_boards;
-    a.draws = d_draws;
-    a.first_action = d_first;
+    a.seeds = (const uint32_t*)dev;
+    a.boards = (int8_t*)(dout + out.off[o_b]);
+    a.draws = (uint32_t*)(dout + out.off[o_d]);
+    a.first_action = (int32_t*)(dout + out.off[o_f]);
     rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, n); });
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out_boards, d_boards, n * c->N, hipMemcpyDeviceToHost, c->stream));
-    if (out_draws) HIP_TRY(hipMemcpyAsync(out_draws, d_draws, n * 4, hipMemcpyDeviceToHost, c->stream));
-    if (out_first_action) HIP_TRY(hipMemcpyAsync(out_first_action, d_first, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return M3_OK;
+    return stage_download(c, out, {out_boards, out_draws, out_first_action}, dout);
 }
 
 int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seeds, const int32_t* n_actions,
@@ -275,50 +348,43 @@ int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t*
               "null buffer");
     int rc0 = check_ids_on_board(c);
     if (rc0) return rc0;
-    for (int64_t i = 0; i < n * c->N; ++i)
-        if (boards[i] < 0) return set_err(M3_ERR_INVALID, "cell value outside [0, 127] at byte %lld", (long long)i);
     HIP_TRY(hipSetDevice(c->device));
     const size_t bytes = n * (size_t)c->N;
-    const size_t need = carve_size({bytes, n * 4ull, n * 4ull, n * 4ull, bytes, n * 4ull, n * 4ull, n * 4ull,
-                                    n * 4ull * c->AW, n * 4ull, n * 4ull});
-    int rc = ensure_scratch(c, need);
+    Image in, out;  // cell values are checked on the device while the boards are staged (k_apply)
+    const int i_b = in.add(bytes), i_s = in.add(n * 4ull), i_na = in.add(n * 4ull), i_a = in.add(n * 4ull);
+    const int o_cnt = out.add(16), o_b = out.add(bytes), o_r = out.add(n * 4ull), o_d = out.add(n * 4ull),
+              o_f = out.add(n * 4ull), o_l = out.add(out_legal_bits ? n * 4ull * c->AW : 0),
+              o_x = out.add(out_next_action ? n * 4ull : 0);
+    char* dev;
+    int rc = stage_begin(c, in, out, n * 4ull, &dev);
     if (rc) return rc;
-    Carve cv{(char*)c->dbuf};
+    char* dout = dev + ((in.total + 255) & ~size_t(255));
+    char* dtail = dout + ((out.total + 255) & ~size_t(255));
+    rc = stage_upload(c, in, {boards, seeds, n_actions, actions}, dev, 16);
+    if (rc) return rc;
     ApplyArgs a{};
     a.shape = c->sdesc;
     a.n = n;
-    int8_t* d_in = cv.take<int8_t>(bytes);
-    uint32_t* d_seeds = cv.take<uint32_t>(n);
-    int32_t* d_na = cv.take<int32_t>(n);
-    int32_t* d_act = cv.take<int32_t>(n);
-    a.boards = d_in;
-    a.seeds = d_seeds;
-    a.n_actions = d_na;
-    a.actions = d_act;
-    a.out_boards = cv.take<int8_t>(bytes);
-    a.reward = cv.take<int32_t>(n);
-    a.draws = cv.take<uint32_t>(n);
-    a.flags = cv.take<uint32_t>(n);
-    a.legal = out_legal_bits ? cv.take<uint32_t>(n * c->AW) : nullptr;
-    a.next_action = out_next_action ? cv.take<int32_t>(n) : nullptr;
-    a.ovf_list = cv.take<uint32_t>(n);
-    a.ovf_count = c->counters;
-    HIP_TRY(hipMemcpyAsync(d_in, boards, bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_seeds, seeds, n * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_na, n_actions, n * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_act, actions, n * 4, hipMemcpyHostToDevice, c->stream));
+    a.boards = (const int8_t*)(dev + in.off[i_b]);
+    a.seeds = (const uint32_t*)(dev + in.off[i_s]);
+    a.n_actions = (const int32_t*)(dev + in.off[i_na]);
+    a.actions = (const int32_t*)(dev + in.off[i_a]);
+    a.out_boards = (int8_t*)(dout + out.off[o_b]);
+    a.reward = (int32_t*)(dout + out.off[o_r]);
+    a.draws = (uint32_t*)(dout + out.off[o_d]);
+    a.flags = (uint32_t*)(dout + out.off[o_f]);
+    a.legal = out_legal_bits ? (uint32_t*)(dout + out.off[o_l]) : nullptr;
+    a.next_action = out_next_action ? (int32_t*)(dout + out.off[o_x]) : nullptr;
+    a.ovf_count = (uint32_t*)(dout + out.off[o_cnt]);  // zeroed by the upload, returned with the outputs
+    a.bad_cells = a.ovf_count + 1;
+    a.ovf_list = (uint32_t*)dtail;
     rc = with_shape(c->shape, [&](auto cf) { return launch_apply<decltype(cf)>(c, a); });
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out_boards, a.out_boards, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(out_reward, a.reward, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(out_draws, a.draws, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(out_flags, a.flags, n * 4, hipMemcpyDeviceToHost, c->stream));
-    if (out_legal_bits)
-        HIP_TRY(hipMemcpyAsync(out_legal_bits, a.legal, n * 4ull * c->AW, hipMemcpyDeviceToHost, c->stream));
-    if (out_next_action)
-        HIP_TRY(hipMemcpyAsync(out_next_action, a.next_action, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return M3_OK;
+    uint32_t cnt[4];
+    rc = stage_download(c, out, {cnt, out_boards, out_reward, out_draws, out_flags, out_legal_bits,
+                                 out_next_action}, dout);
+    if (rc) return rc;
+    return cnt[1] ? bad_cells_error(cnt[1]) : M3_OK;
 }
 
 int m3_legal_actions(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* out_legal_bits) {
@@ -328,18 +394,20 @@ int m3_legal_actions(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* out_l
     int rc0 = check_ids_on_board(c);
     if (rc0) return rc0;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t bytes = n * (size_t)c->N;
-    int rc = ensure_scratch(c, carve_size({bytes, n * 4ull * c->AW}));
+    Image in, out;
+    in.add(n * (size_t)c->N);
+    out.add(n * 4ull * c->AW);
+    char* dev;
+    int rc = stage_begin(c, in, out, 0, &dev);
     if (rc) return rc;
-    Carve cv{(char*)c->dbuf};
-    int8_t* d_in = cv.take<int8_t>(bytes);
-    uint32_t* d_out = cv.take<uint32_t>(n * c->AW);
-    HIP_TRY(hipMemcpyAsync(d_in, boards, bytes, hipMemcpyHostToDevice, c->stream));
-    rc = with_shape(c->shape, [&](auto cf) { return launch_legal<decltype(cf)>(c, n, d_in, d_out); });
+    char* dout = dev + ((in.total + 255) & ~size_t(255));
+    rc = stage_upload(c, in, {boards}, dev);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out_legal_bits, d_out, n * 4ull * c->AW, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return M3_OK;
+    rc = with_shape(c->shape, [&](auto cf) {
+        return launch_legal<decltype(cf)>(c, n, (const int8_t*)dev, (uint32_t*)dout);
+    });
+    if (rc) return rc;
+    return stage_download(c, out, {out_legal_bits}, dout);
 }
 
 // ---- rollouts ---------------------------------------------------------------
@@ -358,14 +426,18 @@ size_t rollout_spill_words(int shape) {
     });
 }
 
-// a.n and the per-rollout buffers set; carves the pool from cv and launches
-int enqueue_rollouts(m3_ctx* c, RolloutArgs a, Carve& cv) {
+// a.n and the per-rollout buffers set; carves the pool from cv and launches.
+// counters: 16 zeroed bytes on the device (nullptr: the context's, zeroed here)
+int enqueue_rollouts(m3_ctx* c, RolloutArgs a, Carve& cv, uint32_t* counters = nullptr) {
     const int64_t cap = rollout_spill_cap(a.n);
-    a.counters = c->counters;
+    if (!counters) {
+        counters = c->counters;
+        HIP_TRY(hipMemsetAsync(counters, 0, 16, c->stream));
+    }
+    a.counters = counters;
     a.ovf_list = cv.take<uint32_t>(a.n);
     a.spill = cv.take<uint32_t>(cap * rollout_spill_words(c->shape));
     a.spill_cap = (uint32_t)cap;
-    HIP_TRY(hipMemsetAsync(c->counters, 0, 16, c->stream));
     return with_shape(c->shape, [&](auto cf) { return launch_rollouts<decltype(cf)>(c, a); });
 }
 
@@ -412,45 +484,39 @@ int m3_rollouts(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seed
               "null buffer");
     int rc0 = check_ids_on_board(c);
     if (rc0) return rc0;
-    for (int64_t i = 0; i < n * c->N; ++i)
-        if (boards[i] < 0) return set_err(M3_ERR_INVALID, "cell value outside [0, 127] at byte %lld", (long long)i);
     HIP_TRY(hipSetDevice(c->device));
     const size_t bytes = n * (size_t)c->N;
-    const size_t need = carve_size({bytes, n * 4ull, n * 4ull, n * 4ull, n * 4ull, n * 4ull, n * 4ull, n * 4ull,
-                                    out_boards ? bytes : 0, n * 4ull,
-                                    rollout_spill_cap(n) * rollout_spill_words(c->shape) * 4ull});
-    int rc = ensure_scratch(c, need);
+    Image in, out;  // cell values are checked on the device while the boards are staged (k_rollout)
+    const int i_b = in.add(bytes), i_s = in.add(n * 4ull), i_na = in.add(n * 4ull), i_rs = in.add(n * 4ull);
+    const int o_cnt = out.add(16), o_g = out.add(n * 4ull), o_st = out.add(n * 4ull), o_d = out.add(n * 4ull),
+              o_f = out.add(n * 4ull), o_b = out.add(out_boards ? bytes : 0);
+    const size_t tail = carve_size({n * 4ull, rollout_spill_cap(n) * rollout_spill_words(c->shape) * 4ull});
+    char* dev;
+    int rc = stage_begin(c, in, out, tail, &dev);
     if (rc) return rc;
-    Carve cv{(char*)c->dbuf};
+    char* dout = dev + ((in.total + 255) & ~size_t(255));
+    char* dtail = dout + ((out.total + 255) & ~size_t(255));
+    rc = stage_upload(c, in, {boards, seeds, n_actions, rollout_seeds}, dev, 16);
+    if (rc) return rc;
     RolloutArgs a{};
     a.shape = c->sdesc;
     a.n = n;
-    int8_t* d_in = cv.take<int8_t>(bytes);
-    uint32_t* d_seeds = cv.take<uint32_t>(n);
-    int32_t* d_na = cv.take<int32_t>(n);
-    uint32_t* d_rs = cv.take<uint32_t>(n);
-    a.boards = d_in;
-    a.seeds = d_seeds;
-    a.n_actions = d_na;
-    a.rseeds = d_rs;
-    a.gain = cv.take<int32_t>(n);
-    a.steps = cv.take<int32_t>(n);
-    a.draws = cv.take<uint32_t>(n);
-    a.flags = cv.take<uint32_t>(n);
-    a.out_boards = out_boards ? cv.take<int8_t>(bytes) : nullptr;
-    HIP_TRY(hipMemcpyAsync(d_in, boards, bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_seeds, seeds, n * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_na, n_actions, n * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_rs, rollout_seeds, n * 4, hipMemcpyHostToDevice, c->stream));
-    rc = enqueue_rollouts(c, a, cv);
+    a.boards = (const int8_t*)(dev + in.off[i_b]);
+    a.seeds = (const uint32_t*)(dev + in.off[i_s]);
+    a.n_actions = (const int32_t*)(dev + in.off[i_na]);
+    a.rseeds = (const uint32_t*)(dev + in.off[i_rs]);
+    a.gain = (int32_t*)(dout + out.off[o_g]);
+    a.steps = (int32_t*)(dout + out.off[o_st]);
+    a.draws = (uint32_t*)(dout + out.off[o_d]);
+    a.flags = (uint32_t*)(dout + out.off[o_f]);
+    a.out_boards = out_boards ? (int8_t*)(dout + out.off[o_b]) : nullptr;
+    Carve cv{dtail};
+    rc = enqueue_rollouts(c, a, cv, (uint32_t*)(dout + out.off[o_cnt]));  // zeroed by the upload
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out_gain, a.gain, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(out_steps, a.steps, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(out_draws, a.draws, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(out_flags, a.flags, n * 4, hipMemcpyDeviceToHost, c->stream));
-    if (out_boards) HIP_TRY(hipMemcpyAsync(out_boards, a.out_boards, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return M3_OK;
+    uint32_t cnt[4];
+    rc = stage_download(c, out, {cnt, out_gain, out_steps, out_draws, out_flags, out_boards}, dout);
+    if (rc) return rc;
+    return cnt[2] ? bad_cells_error(cnt[2]) : M3_OK;
 }
 
 // ---- env ------------------------------------------------------------------

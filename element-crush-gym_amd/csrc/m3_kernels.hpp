@@ -64,6 +64,10 @@ constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 #define M3_RESET_KCAP 454
 #endif
 constexpr uint32_t RESET_KCAP = M3_RESET_KCAP;
+// A reset stops after this many rounds of BoardV2.__init__'s redraw loop (boardv2.py:23-27) and
+// flags M3_FLAG_RESET_CAP: only two-colour boards get near it (a 16x16x2 reset can need more than
+// 10,000 rounds; the reference keeps going), and a GPU lane must end.
+constexpr uint32_t RESET_ROUND_CAP = 1u << 14;
 
 // Per-shape step-kernel geometry: boards (lanes) per workgroup and the
 // match-group table capacity, sized so staging + table fit the 160 KB LDS.
@@ -92,6 +96,10 @@ struct KS {
 #define M3_CONT_WPS M3_STEP_WPS
 #endif
     static constexpr int CONT_WPS = CF::N > 128 ? 1 : M3_CONT_WPS;
+    // k_env_cont's persistent waves per shard launch (each loops over the paused-step queue)
+#ifndef M3_CONT_WAVES
+#define M3_CONT_WAVES 1024
+#endif
     static constexpr uint32_t SPILL_RECORDS = 4096;  // spill pool records per shard
     // The env step's RNG is the register-only MT19937 chain from the board's
     // (seed, mt[397]) -- 4 B of per-board state (a per-board stream cache of
@@ -117,6 +125,18 @@ struct KS {
     static constexpr int CASCADE_LIMIT = CF::N > 128 ? M3_CASCADE_LIMIT16 : M3_CASCADE_LIMIT;
 };
 
+// LDS pointers carry their address space, so table accesses compile to ds_*
+// instructions: a generic pointer that may point at either the LDS table or
+// the global spill pool made the compiler emit flat loads, and every wait on a
+// flat load also waits for all of the wave's global memory traffic.
+#ifdef __HIP_DEVICE_COMPILE__
+#define M3_LDS_AS __attribute__((address_space(3)))
+#else
+#define M3_LDS_AS
+#endif
+typedef M3_LDS_AS uint32_t lds_u32;
+__device__ __forceinline__ lds_u32* as_lds(uint32_t* p) { return (lds_u32*)p; }
+
 // Per-lane match-group table (see m3_rules.hpp, match_scan): the first CAP
 // groups in LDS, entry (g, h|v, word i) of lane l at tab[((g*2 + hv)*W + i)*LANES + l]
 // (consecutive lanes hit consecutive dwords: conflict-free). A board that
@@ -130,7 +150,7 @@ struct LdsTable {
     static constexpr int W = CF::W;
     static constexpr int BLOCK = LANES;
     static constexpr int WORDS = CAP * 2 * W * BLOCK;
-    uint32_t* tab;  // already offset by threadIdx.x
+    lds_u32* tab;  // already offset by threadIdx.x
     __device__ __forceinline__ typename CF::Bd get_h(int g) const {
         typename CF::Bd r;
 #pragma unroll
@@ -161,7 +181,7 @@ struct LdsStore {
     static constexpr int BLOCK = LANES;
     static constexpr int WORDS = LCAP * 2 * W * BLOCK;
     static constexpr int SPILL_WORDS = (CF::MAXG - LCAP) * 2 * W;  // per pool record
-    uint32_t* tab;        // already offset by threadIdx.x
+    lds_u32* tab;         // already offset by threadIdx.x
     uint32_t* spill;      // nullable: pool of records
     uint32_t* pool_next;  // pool allocation counter
     uint32_t pool_cap;
@@ -281,6 +301,32 @@ __device__ __forceinline__ void block_copy_in(const int8_t* __restrict__ g, uint
     uint4* d4 = reinterpret_cast<uint4*>(lds);
     for (int i = threadIdx.x; i < n16; i += BLOCK) d4[i] = s4[i];
     for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) lds[i] = (uint8_t)g[i];
+}
+
+// the same copy for host-supplied boards: also reports whether any byte of the
+// thread's share has bit 7 set (a cell value outside [0, 127], include/m3.h)
+template <int BLOCK>
+__device__ __forceinline__ bool block_copy_in_checked(const int8_t* __restrict__ g, uint8_t* lds, int bytes) {
+    const int n16 = bytes >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(g);
+    uint4* d4 = reinterpret_cast<uint4*>(lds);
+    uint32_t hi = 0u;
+    for (int i = threadIdx.x; i < n16; i += BLOCK) {
+        const uint4 v = s4[i];
+        hi |= v.x | v.y | v.z | v.w;
+        d4[i] = v;
+    }
+    for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) {
+        const uint8_t v = (uint8_t)g[i];
+        hi |= v;
+        lds[i] = v;
+    }
+    return (hi & 0x80808080u) != 0u;
+}
+
+// count the waves that saw a bad cell (one atomic per such wave)
+__device__ __forceinline__ void flag_bad_cells(bool bad, uint32_t* counter) {
+    if (counter && __any((int)bad) && __lane_id() == 0) atomicAdd(counter, 1u);
 }
 
 template <int BLOCK>
@@ -414,6 +460,7 @@ struct ApplyArgs {
     int32_t* next_action;  // nullable
     uint32_t* ovf_count;
     uint32_t* ovf_list;
+    uint32_t* bad_cells;   // nullable: waves that saw a cell value outside [0, 127]
 };
 }  // namespace m3k
 using m3k::ApplyArgs;
@@ -453,7 +500,7 @@ __global__ void __launch_bounds__(KS<CF>::B) k_apply(ApplyArgs a) {
     const int NC = dm.cells();
     const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
     const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
-    block_copy_in<KS<CF>::B>(a.boards + b0 * NC, lds, nb * NC);
+    flag_bad_cells(block_copy_in_checked<KS<CF>::B>(a.boards + b0 * NC, lds, nb * NC), a.bad_cells);
     lds_sync();
     const int t = threadIdx.x;
     if (t < nb) {
@@ -463,7 +510,7 @@ __global__ void __launch_bounds__(KS<CF>::B) k_apply(ApplyArgs a) {
         const uint32_t s = a.seeds[b];
         ChainMT rng;
         rng.init(s, mt_state397(s));
-        LdsTable<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};  // overflow -> k_apply_fix
+        LdsTable<CF, KS<CF>::GCAP, KS<CF>::B> st{as_lds(gtab + t)};  // overflow -> k_apply_fix
         if (!apply_and_emit<CF>(P, a, b, rng, st, dm)) {
             const uint32_t slot = atomicAdd(a.ovf_count, 1u);
             a.ovf_list[slot] = (uint32_t)b;
@@ -903,15 +950,19 @@ __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
             typename CF::Bd P[CF::NP], mask;
 #pragma unroll
             for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+            uint32_t rounds = 0;
             if constexpr (CF::DYN) {
                 fill_round_frame<CF>(P, mt, nullptr, dm);                              // boardv2.py:21
-                while (get_match_mask<CF>(P, mask)) fill_round_frame<CF>(P, mt, &mask, dm);  // :23-27
+                while (get_match_mask<CF>(P, mask) && ++rounds < RESET_ROUND_CAP)    // :23-27
+                    fill_round_frame<CF>(P, mt, &mask, dm);
             } else {
                 fill_round<CF>(P, mt, nullptr);                              // boardv2.py:21
-                while (get_match_mask<CF>(P, mask)) fill_round<CF>(P, mt, &mask);  // boardv2.py:23-27
+                while (get_match_mask<CF>(P, mask) && ++rounds < RESET_ROUND_CAP)  // boardv2.py:23-27
+                    fill_round<CF>(P, mt, &mask);
             }
             const int64_t ob = (int64_t)slot * a.sstride + b;
             init_outputs<CF>(a, b, ob, seed, m397, mt.draws(), P, dm);
+            if (rounds >= RESET_ROUND_CAP && a.flags) a.flags[b] |= FLAG_RESET_CAP;
             init_store_board<CF>(a, ob, P, dm);
             long_reset = mt.draws() >= 624u;
         }
@@ -1054,7 +1105,8 @@ struct EnvArgs {
     uint32_t* legal;  // nullable
     int32_t* packed;  // nullable: reward<<2 | trunc<<1 | done for the RCCL gather
     uint32_t* counters;  // this step's block: [0] overflow count, [1] prefetch count, [2] prefetch overflow
-                         // count, [3] spill records used, [4] continuation records
+                         // count, [3] spill records used, [4] continuation records, [5] records taken
+                         // by k_env_cont
     uint32_t* spill;     // group-table spill pool of the shard
     uint32_t* stats;     // [0] step recomputes
     uint32_t* ovf_list;
@@ -1225,12 +1277,12 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
 #ifdef M3_PHASE_PROF
     M3_PROF_LDS(KS<CF>::B)
     Prof<LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>> st;
-    st.tab = gtab + t;
+    st.tab = as_lds(gtab + t);
     st.w = prof_s[t >> 6];
     const bool live = ((t & ~63) < nb);
     if (live) st.begin();
 #else
-    LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{gtab + t};
+    LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{as_lds(gtab + t)};
 #endif
     st.spill = a.spill;
     st.pool_next = &a.counters[3];
@@ -1291,9 +1343,15 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
 }
 
 // Finish the steps k_env_step paused (their cascade ran past KS::CASCADE_LIMIT
-// inner iterations): the long cascades of a launch, packed densely into waves
-// instead of holding every lane of their k_env_step wave idle. Grid-stride
-// over the records; each board is written straight to nxt.
+// inner iterations, or it settled on a board with no legal move). The paused
+// boards are the long cascades of a launch, and their remaining iteration
+// counts still differ a lot: a wave that took 64 of them and ran each to the
+// end would run as long as its longest. Instead every lane advances its board
+// by ONE cascade iteration per trip (apply_cascade_ex with limit 1) and, when
+// that board is finished (bookkeeping + board written straight to nxt), takes
+// the next record from the launch's queue (one wave-aggregated atomic per trip
+// that needs records, counter block [5]), so the waves stay full until the
+// queue drains. Persistent grid: a fixed number of waves loops over the records.
 template <class CF>
 __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont(EnvArgs a) {
     using K = KS<CF>;
@@ -1302,34 +1360,59 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont(EnvArg
     __builtin_amdgcn_s_setprio(3);
     __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
     const uint32_t cnt = a.counters[4];
-    LdsStore<CF, K::GCAP, K::B> st{tab + threadIdx.x};
+    LdsStore<CF, K::GCAP, K::B> st{as_lds(tab + threadIdx.x)};
     st.spill = a.spill;
     st.pool_next = &a.counters[3];
     st.pool_cap = K::SPILL_RECORDS;
     const int64_t cs = a.cont_stride;
-    for (uint32_t q = blockIdx.x * K::B + threadIdx.x; q < cnt; q += gridDim.x * K::B) {
-        const uint32_t* rec = a.cont + q;
-        const int64_t b = rec[0];
-        typename CF::Bd P[CF::NP];
-        typename K::Rng rng;
-        int r;
-        uint32_t f;
-        EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
-        const int mv = a.moves[b], sc0 = a.score[b];
-        typename CF::Bd HL, VL;
-        const bool dead = (f & FLAG_CONT_DEAD) != 0;  // settled with no legal move: continue at the shuffle
-        f &= ~FLAG_CONT_DEAD;
-        const typename CF::Dim dm(a.shape);
-        apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, -1, dead, dm);
-        const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm);
-        if (!ok) {
-            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-            a.ovf_list[slot] = (uint32_t)b;
-        } else {
-            constexpr int NW = (CF::N + 3) / 4;
-            uint32_t cw[NW];
-            words_from_planes<CF>(P, cw);
-            store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.nxt + b * CF::N), cw);
+    const typename CF::Dim dm(a.shape);
+    const int lane = (int)__lane_id();
+    typename CF::Bd P[CF::NP], HL, VL;
+    typename K::Rng rng;
+    int r = 0;
+    uint32_t f = 0u;
+    int64_t b = -1;        // this lane's board (-1: none)
+    bool settled = false;  // its next trip starts at the legal set (a dead board: the shuffle)
+    bool exhausted = false;
+    for (;;) {
+        const bool need = b < 0 && !exhausted;
+        const uint64_t nm = __ballot(need);
+        if (nm) {  // lanes without a board take the next records
+            const int leader = __ffsll((unsigned long long)nm) - 1;
+            uint32_t base = 0u;
+            if (lane == leader) base = atomicAdd(&a.counters[5], (uint32_t)__popcll(nm));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t q = base + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
+                if (q < cnt) {
+                    const uint32_t* rec = a.cont + q;
+                    b = rec[0];
+                    EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
+                    settled = (f & FLAG_CONT_DEAD) != 0;  // settled with no legal move: continue at the shuffle
+                    f &= ~FLAG_CONT_DEAD;
+                } else {
+                    exhausted = true;
+                }
+            }
+        }
+        if (!__any(b >= 0)) break;
+        if (b >= 0) {
+            const int c = apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, 1, settled, dm);
+            settled = false;
+            if (c != CAS_PAUSED) {  // finished (or flagged for the exact recompute)
+                const int mv = a.moves[b], sc0 = a.score[b];
+                const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm);
+                if (!ok) {
+                    const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+                    a.ovf_list[slot] = (uint32_t)b;
+                } else {
+                    constexpr int NW = (CF::N + 3) / 4;
+                    uint32_t cw[NW];
+                    words_from_planes<CF>(P, cw);
+                    store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.nxt + b * CF::N), cw);
+                }
+                b = -1;
+            }
         }
     }
 }
@@ -1393,7 +1476,7 @@ struct RolloutArgs {
     uint32_t* draws;           // global-stream draws since its last seed when the rollout ends
     uint32_t* flags;           // OR of the steps' M3_FLAG_*
     int8_t* out_boards;        // nullable: terminal boards
-    uint32_t* counters;        // [0] overflow count, [1] spill records taken
+    uint32_t* counters;        // [0] overflow count, [1] spill records taken, [2] waves with a bad cell
     uint32_t* ovf_list;
     uint32_t* spill;
     uint32_t spill_cap;
@@ -1455,13 +1538,13 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_rollout(Rollout
     const int NC = dm.cells();
     const int64_t b0 = (int64_t)blockIdx.x * K::B;
     const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
-    block_copy_in<K::B>(a.boards + b0 * NC, lds, nb * NC);
+    flag_bad_cells(block_copy_in_checked<K::B>(a.boards + b0 * NC, lds, nb * NC), &a.counters[2]);
     lds_sync();
     const int t = threadIdx.x;
     typename CF::Bd P[CF::NP];
     if (t < nb) lds_to_planes<CF>(lds, t, P, dm);
     lds_sync();
-    LdsStore<CF, K::GCAP, K::B> st{stage_tab + t};
+    LdsStore<CF, K::GCAP, K::B> st{as_lds(stage_tab + t)};
     st.spill = a.spill;
     st.pool_next = &a.counters[1];
     st.pool_cap = a.spill_cap;
@@ -1512,9 +1595,11 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_rollout_fix(RolloutArgs a) {
 constexpr int N_SPECIALISED = 2;
 // Specialised shapes first (ids 0..N_SPECIALISED-1), then the frame configs
 // FCfg<2..4> (ids N_SPECIALISED + BITS - 2) for every other supported shape:
-// rows and columns 3..16, types 3..15. (types = 2: a refill almost never
-// leaves a 2-colour board without a match, so the reference's cascade does
-// not end in practice; types = 1: its reset never ends.)
+// rows and columns 3..16, types 2..15. (types = 2: from about 7x7 up a refill
+// of two colours almost always leaves a match, so the reference's cascade
+// does not return -- steps here stop at CASCADE_CAP refills and flag it -- and
+// a large board's reset can take millions of draws -- stopped at
+// RESET_ROUND_CAP rounds and flagged; types = 1: the reset never ends.)
 int shape_id(int r, int c, int t) {
     int id = 0;
 #define X(R_, C_, T_)                                 \
@@ -1522,7 +1607,7 @@ int shape_id(int r, int c, int t) {
     ++id;
     M3_SHAPES(X)
 #undef X
-    if (r >= 3 && r <= 16 && c >= 3 && c <= 16 && t >= 3 && t <= 15) return N_SPECIALISED + bits_for_types(t) - 2;
+    if (r >= 3 && r <= 16 && c >= 3 && c <= 16 && t >= 2 && t <= 15) return N_SPECIALISED + bits_for_types(t) - 2;
     return -1;
 }
 
@@ -1540,7 +1625,11 @@ struct m3_ctx {
     // stateless scratch
     void* dbuf = nullptr;
     size_t dcap = 0;
-    uint32_t* counters = nullptr;  // [0] overflow count
+    // pinned host staging of the host-buffer calls: inputs go up as one image, outputs come back
+    // as one image (one copy each way per call, include/m3.h "stateless batch calls")
+    void* hbuf = nullptr;
+    size_t hcap = 0;
+    uint32_t* counters = nullptr;  // rollouts: [0] overflow count, [1] spill records, [2] bad-cell waves
 };
 
 struct m3_env {
@@ -1631,8 +1720,7 @@ int grid_for(int64_t n) { return (int)((n + KS<CF>::B - 1) / KS<CF>::B); }
 
 template <class CF>
 int launch_apply(m3_ctx* c, const ApplyArgs& a) {
-    if (a.n == 0) return M3_OK;
-    HIP_TRY(hipMemsetAsync(a.ovf_count, 0, sizeof(uint32_t), c->stream));
+    if (a.n == 0) return M3_OK;  // (*a.ovf_count and *a.bad_cells are zero: the caller's upload)
     hipLaunchKernelGGL(k_apply<CF>, dim3(grid_for<CF>(a.n)), dim3(KS<CF>::B), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_apply_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
@@ -1755,9 +1843,10 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
     HIP_TRY(hipGetLastError());
     if constexpr (KS<CF>::CASCADE_LIMIT >= 0) {
-        // grid-strides over the device-side count of paused steps: sized for their usual share (~20 % at limit 2)
-        const int64_t g = ((int64_t)(sh.n * 0.25) + KS<CF>::B - 1) / KS<CF>::B;
-        hipLaunchKernelGGL(k_env_cont<CF>, dim3((unsigned)(g > 0 ? g : 1)), dim3(KS<CF>::B), 0, st, a);
+        // persistent waves over the device-side queue of paused steps (~19 % of the boards at limit 2)
+        int64_t g = ((int64_t)(sh.n * 0.2) + KS<CF>::B - 1) / KS<CF>::B;
+        g = g < 1 ? 1 : (g > M3_CONT_WAVES ? M3_CONT_WAVES : g);
+        hipLaunchKernelGGL(k_env_cont<CF>, dim3((unsigned)g), dim3(KS<CF>::B), 0, st, a);
         HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);

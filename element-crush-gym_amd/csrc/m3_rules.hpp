@@ -55,13 +55,16 @@ enum : uint32_t {
     FLAG_GROUP_OVERFLOW = 0x40u, // internal: more match groups than the fast table holds; recomputed
     FLAG_RECOMPUTE = FLAG_RNG_OVERFLOW | FLAG_GROUP_OVERFLOW,
     FLAG_CASCADE_CAP = 0x100u, // cascade stopped after CASCADE_CAP refills (reference: unbounded)
+    FLAG_RESET_CAP = 0x200u,   // reset stopped after RESET_ROUND_CAP redraw rounds (reference: unbounded)
 };
 // Refill-and-rematch passes one step may run. The reference loops until a
-// refill leaves no match (boardv2.py:138-202); with few tile types on a large
-// board (types = 2) that practically never happens, and a GPU lane must end.
-// Steps of the supported shapes use 1-10 passes; the cap is a
-// safety bound, flagged when hit (parity undefined there, as at the shuffle cap).
-constexpr int CASCADE_CAP = 1024;
+// refill leaves no match (boardv2.py:138-202); with two tile types on a board
+// of about 7x7 or more that practically never happens (tests/golden/types2.npz
+// records it), and a GPU lane must end.
+// Steps of the headline shapes use 1-10 passes, two-colour 6x6
+// steps up to ~10,000 (types2.npz); the cap is a safety bound above those,
+// flagged when hit (parity undefined there, as at the shuffle cap).
+constexpr int CASCADE_CAP = 1 << 16;
 // An RNG that raises `overflow` after a fixed number of draws (ChainMT: 624)
 // bounds the cascade by itself -- every pass that continues refills >= 3
 // cleared cells -- so the specialised shapes on such a stream skip the pass

@@ -25,6 +25,7 @@ FLAG_SHUFFLE_CAP = 0x04
 FLAG_NO_LEGAL = 0x08
 FLAG_SHUFFLED = 0x10
 FLAG_CASCADE_CAP = 0x100
+FLAG_RESET_CAP = 0x200
 
 ENV_BOARDS, ENV_REWARD, ENV_DONE, ENV_TRUNCATED, ENV_SCORE, ENV_MOVES, ENV_FLAGS, ENV_NEXT_ACTION, \
     ENV_LEGAL, ENV_SEEDS, ENV_DRAWS, ENV_GATHERED = range(12)

@@ -48,7 +48,8 @@ extern "C" {
 #define M3_FLAG_SHUFFLE_CAP 0x04u /* dead-board shuffle cycled past the cap: reference hangs (boardv2.py:188-194) */
 #define M3_FLAG_NO_LEGAL 0x08u    /* no legal action to sample: reference raises in np.random.choice */
 #define M3_FLAG_SHUFFLED 0x10u    /* the dead-board shuffle ran */
-#define M3_FLAG_CASCADE_CAP 0x100u /* cascade stopped after 1024 refills: the reference keeps going (types = 2 boards) */
+#define M3_FLAG_CASCADE_CAP 0x100u /* cascade stopped after 65536 refills: the reference keeps going (types = 2 boards) */
+#define M3_FLAG_RESET_CAP 0x200u   /* reset stopped after 16384 redraw rounds: the reference keeps going (large types = 2 boards) */
 
 typedef struct m3_ctx m3_ctx;
 typedef struct m3_env m3_env;

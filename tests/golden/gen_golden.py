@@ -22,6 +22,8 @@ Files written:
                   reset at done with and without a seed), bookkeeping restated over the reference
                   BoardV2 (env.py cannot run at the snapshot): obs/reward/done/truncated per step
   shapes.npz      init / legal / steps / episodes for BoardConfigs other than 9x9x6 and 16x16x8
+  types2.npz      BoardConfig(types=2): steps / episodes on 4x4, 5x5, 6x6 (where the reference's
+                  cascade returns), resets and legal sets on 9x9, 12x7
                   (square, rows > columns, columns = 3 -- the decode quirk -- and few types), and
                   for rows < columns, where the reference's legal_actions / apply_action raise
                   IndexError, the init boards plus that error
@@ -67,13 +69,13 @@ def draws_since_seed(seed: int) -> int:
     fresh = np.random.RandomState(seed).get_state()
     if pos == 624 and np.array_equal(fresh[1], key):
         return 0
-    for t in range(1, 16):
-        d = (t - 1) * 624 + pos
-        rs = np.random.RandomState(seed)
-        rs._bit_generator.random_raw(d)
+    rs = np.random.RandomState(seed)
+    rs._bit_generator.random_raw(pos)  # d = (t - 1) * 624 + pos for t = 1, 2, ...
+    for t in range(1, 4096):
         s2 = rs.get_state()
         if s2[2] == pos and np.array_equal(s2[1], key):
-            return d
+            return (t - 1) * 624 + pos
+        rs._bit_generator.random_raw(624)
     raise RuntimeError("could not determine draw count")
 
 
@@ -634,8 +636,81 @@ def gen_shapes(pool):
     np.savez_compressed(os.path.join(OUT, "shapes.npz"), **out)
 
 
+# types = 2 (BoardConfig(types=2): TM 3, H 4, V 8, B 12, M 16). The reference resets every size,
+# but on boards from about 7x7 up a refill of two colours almost always leaves a new match, so
+# its cascade (boardv2.py:138-202) does not return (and a 16x16x2 reset can take millions of draws):
+# steps and episodes are recorded for the small
+# boards where it does, resets and legal sets for the large ones, plus how many first moves of
+# seeded play return within 3 s there.
+TYPES2_PLAY = [(5, 5, 2), (4, 4, 2), (6, 6, 2)]
+TYPES2_RESET = [(9, 9, 2), (12, 7, 2)]
+
+
+def _first_move_returns(args):
+    R, C, T, seed = args
+    signal.signal(signal.SIGALRM, _alarm)
+    signal.alarm(3)
+    try:
+        cfg = BoardConfig(seed=int(seed), rows=R, columns=C, types=T)
+        b = BoardV2(20, cfg)
+        np.random.seed(cfg.seed)
+        b.apply_action(int(np.random.choice(b.legal_actions)))
+        return 1
+    except _Timeout:
+        return 0
+    finally:
+        signal.alarm(0)
+
+
+def gen_types2(pool):
+    rng = np.random.default_rng(2222)
+    out = {}
+    for (R, C, T) in TYPES2_PLAY + TYPES2_RESET:
+        tag = f"{R}x{C}x{T}"
+        cfg = BoardConfig(seed=1, rows=R, columns=C, types=T)
+        seeds = np.concatenate([np.arange(1, 125), [2**31 - 2, 2**32 - 1, 123456789, 987654321]]).astype(np.uint64)
+        res = pool.map(_init_one, [(R, C, T, s) for s in seeds])
+        out[f"init_seeds_{tag}"] = seeds
+        out[f"init_boards_{tag}"] = np.array([r[0] for r in res])
+        out[f"init_draws_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        boards = [r[0].astype(np.int64) for r in res[:60]]
+        for _ in range(60):
+            b = rng.integers(1, T + 1, size=(R, C))
+            for _ in range(rng.integers(0, 4)):
+                b[rng.integers(0, R), rng.integers(0, C)] = [cfg.h_line, cfg.v_line, cfg.bomb, cfg.mega_token,
+                                                             0][rng.integers(0, 5)]
+            boards.append(b)
+        out[f"legal_boards_{tag}"] = np.array(boards, dtype=np.int8)
+        out[f"legal_{tag}"] = np.array([legal_bits(cfg, b) for b in boards], dtype=np.uint8)
+        if (R, C, T) in TYPES2_RESET:
+            ret = pool.map(_first_move_returns, [(R, C, T, s) for s in range(1, 17)])
+            out[f"first_move_returns_{tag}"] = np.array(ret, dtype=np.uint8)
+            continue
+        cases = step_cases(R, C, T, rng, 300)
+        res = pool.map(_step_case, [(R, C, T, b, s, na, a) for (b, s, na, a) in cases], chunksize=8)
+        out[f"step_board_{tag}"] = np.array([c[0] for c in cases], dtype=np.int8)
+        out[f"step_seed_{tag}"] = np.array([c[1] for c in cases], dtype=np.uint32)
+        out[f"step_n_actions_{tag}"] = np.array([c[2] for c in cases], dtype=np.int32)
+        out[f"step_action_{tag}"] = np.array([c[3] for c in cases], dtype=np.int32)
+        out[f"step_next_{tag}"] = np.array([r[0] for r in res])
+        out[f"step_reward_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        out[f"step_draws_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+        eseeds = np.arange(1, 81, dtype=np.uint64)
+        res = pool.map(_episode, [(R, C, T, s, 20) for s in eseeds], chunksize=2)
+        keep = [i for i, r in enumerate(res) if r is not None][:48]
+        eseeds, res = eseeds[keep], [res[i] for i in keep]
+        out[f"ep_seeds_{tag}"] = eseeds
+        out[f"ep_init_{tag}"] = np.array([r[0] for r in res])
+        out[f"ep_actions_{tag}"] = np.array([r[1] for r in res], dtype=np.int16)
+        out[f"ep_rewards_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+        out[f"ep_draws_{tag}"] = np.array([r[3] for r in res], dtype=np.int16)
+        out[f"ep_final_{tag}"] = np.array([r[4][-1] for r in res])
+    np.savez_compressed(os.path.join(OUT, "types2.npz"), **out)
+
+
 def main():
-    which = sys.argv[1:] or ["prng", "matches", "legal", "init", "steps", "episodes", "shuffle", "env", "shapes"]
+    which = sys.argv[1:] or ["prng", "matches", "legal", "init", "steps", "episodes", "shuffle", "env", "shapes",
+                             "types2"]
     with Pool(8) as pool:
         for w in which:
             print("generating", w, flush=True)
@@ -657,6 +732,8 @@ def main():
                 gen_env(pool)
             elif w == "shapes":
                 gen_shapes(pool)
+            elif w == "types2":
+                gen_types2(pool)
 
 
 if __name__ == "__main__":

@@ -40,10 +40,11 @@ def test_loads_and_reports_shapes():
     L = _native.lib()
     assert L.m3_abi_version() == 1
     assert _native.supported(9, 9, 6) and _native.supported(16, 16, 8)
-    # any other BoardConfig in the 16 x 16 frame: rows / columns 3..16, types 3..15
+    # any other BoardConfig in the 16 x 16 frame: rows / columns 3..16, types 2..15
     assert _native.supported(7, 7, 5) and _native.supported(3, 3, 3) and _native.supported(16, 3, 15)
+    assert _native.supported(9, 9, 2) and _native.supported(5, 5, 2)
     assert _native.supported(8, 10, 5)  # rows < columns: resets only (the reference raises on a step)
-    for bad in ((2, 9, 6), (9, 17, 6), (17, 9, 6), (9, 9, 2), (9, 9, 16), (9, 9, 1)):
+    for bad in ((2, 9, 6), (9, 17, 6), (17, 9, 6), (9, 9, 16), (9, 9, 1)):
         assert not _native.supported(*bad), bad
     a, w = np.zeros(1, np.int32), np.zeros(1, np.int32)
     _native.check(L.m3_action_space(9, 9, _native.ptr(a), _native.ptr(w)))

@@ -294,3 +294,27 @@ def test_c4_262144_boards_autoreset_properties():
     chk = bench.oracle_sample_check(env, (16, 16, 8), 20, goal, 1, n, 20, idx=idx)
     assert chk["boards"] == len(idx) and chk["mismatches"] == 0, chk
     env.close()
+
+
+def test_abi_rejects_bad_cells_on_device(ctxs):
+    """A cell byte outside [0, 127] (int8 < 0) handed straight to the C ABI is caught while the
+    boards are staged on the device (no host pass over the bytes): M3_ERR_INVALID."""
+    c = ctxs["9x9x6"]
+    n = 300
+    seeds = np.arange(1, n + 1, dtype=np.uint32)
+    b, _, fa = c.init_boards(seeds)
+    b = np.ascontiguousarray(b.reshape(n, -1))
+    b[257, 40] = -3  # fifth wave
+    na = np.full(n, 20, np.int32)
+    fa = np.ascontiguousarray(fa, dtype=np.int32)
+    outs = [np.empty(n * 81, np.int8)] + [np.empty(n, np.int32) for _ in range(3)]
+    routs = [np.empty(n, np.int32) for _ in range(4)]  # every buffer outlives the calls
+    P = _native.ptr
+    L = _native.lib()
+    rc = L.m3_apply_actions(c.handle, n, P(b), P(seeds), P(na), P(fa), *[P(o) for o in outs], None, None)
+    assert rc == -1 and b"outside [0, 127]" in L.m3_last_error()
+    rc = L.m3_rollouts(c.handle, n, P(b), P(seeds), P(na), P(seeds), *[P(o) for o in routs], None)
+    assert rc == -1
+    b[257, 40] = 3  # a valid value: both calls succeed again on the same context
+    _native.check(L.m3_apply_actions(c.handle, n, P(b), P(seeds), P(na), P(fa), *[P(o) for o in outs], None, None))
+    _native.check(L.m3_rollouts(c.handle, n, P(b), P(seeds), P(na), P(seeds), *[P(o) for o in routs], None))

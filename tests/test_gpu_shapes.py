@@ -153,3 +153,56 @@ def test_frame_rollouts_and_autoreset_vs_oracle():
     assert (env.observations() == fresh).all() and (env.next_actions() == first).all()
     env.close()
     ctx.close()
+
+
+def test_two_types_golden(golden):
+    """BoardConfig(types=2) against tests/golden/types2.npz: resets and legal sets on 4x4 .. 12x7,
+    apply_action transitions and seeded random_task episodes on 4x4, 5x5 and 6x6 (where the
+    reference's cascade returns)."""
+    g = golden("types2")
+    tags = _tags(g, "init_seeds_")
+    assert {"4x4x2", "5x5x2", "6x6x2", "9x9x2", "12x7x2"} <= set(tags)
+    for tag in tags:
+        R, C, T = _shape(tag)
+        ctx = _native.Context(R, C, T)
+        boards, draws, _ = ctx.init_boards(g["init_seeds_" + tag].astype(np.uint32))
+        assert (boards == g["init_boards_" + tag]).all(), tag
+        assert (draws == g["init_draws_" + tag]).all(), tag
+        assert (unpack(ctx.legal_bits(g["legal_boards_" + tag]), ctx.A) == g["legal_" + tag]).all(), tag
+        if "step_board_" + tag in g.files:
+            ok = g["step_draws_" + tag] != -2
+            r = ctx.apply_actions(g["step_board_" + tag][ok], g["step_seed_" + tag][ok],
+                                  g["step_n_actions_" + tag][ok], g["step_action_" + tag][ok])
+            assert (r["boards"] == g["step_next_" + tag][ok]).all(), tag
+            assert (r["reward"] == g["step_reward_" + tag][ok]).all(), tag
+            live = g["step_draws_" + tag][ok] >= 0
+            assert (r["draws"][live] == g["step_draws_" + tag][ok][live]).all(), tag
+            seeds = g["ep_seeds_" + tag].astype(np.uint32)
+            env = BatchedMatch3Env(len(seeds), R, C, T, num_moves=20, env_goal=BIG, seeds=seeds, autoreset=False)
+            assert (env.observations() == g["ep_init_" + tag]).all(), tag
+            for m in range(20):
+                assert (env.next_actions() == g["ep_actions_" + tag][:, m]).all(), (tag, m)
+                env.step()
+                assert (env.rewards() == g["ep_rewards_" + tag][:, m]).all(), (tag, m)
+            assert (env.observations() == g["ep_final_" + tag]).all(), tag
+            env.close()
+        ctx.close()
+
+
+def test_two_types_large_board_steps_return_flagged(golden):
+    """9x9x2: the reference's first move of seeded play mostly never returns (types2.npz records
+    which of seeds 1..16 did within 3 s); here every step returns, and a step whose cascade ran
+    into the 65,536-refill cap says so (M3_FLAG_CASCADE_CAP, parity undefined there; 6x6x2 steps of the
+    fixture need up to ~10,000 refills, which the cap leaves exact)."""
+    g = golden("types2")
+    assert g["first_move_returns_9x9x2"].sum() < 16  # the reference hangs on some
+    n = 512
+    env = BatchedMatch3Env(n, 9, 9, 2, num_moves=20, env_goal=BIG, seed_base=1, autoreset=False)
+    env.step()
+    f = env.flags()
+    capped = (f & _native.FLAG_CASCADE_CAP) != 0
+    assert capped.any() and env.observations().shape == (n, 9, 9)
+    obs = env.observations()
+    assert np.isin(obs[~capped], [1, 2, 4, 8, 12, 16]).all()  # tiles 1..2, H 4, V 8, B 12, M 16 (TM 3)
+    assert np.isin(obs[capped], [0, 1, 2, 4, 8, 12, 16]).all()  # (a capped cascade stops with its holes)
+    env.close()

@@ -86,3 +86,37 @@ def test_shuffle_path(golden, tag):
             assert f & FLAG_SHUFFLE_CAP
         n_shuffled += bool(f & FLAG_SHUFFLED)
     assert n_shuffled > 100
+
+
+@pytest.mark.parametrize("fixture", ["shapes", "types2"])
+def test_other_board_configs(golden, fixture):
+    """Every other BoardConfig the fixtures hold (shapes.npz: square, rows > columns, 3 and 15
+    types; types2.npz: two tile types), through the oracle: resets, legal sets, transitions and
+    seeded episodes."""
+    g = golden(fixture)
+    tags = sorted({k[len("init_seeds_"):] for k in g.files if k.startswith("init_seeds_")})
+    assert tags
+    for tag in tags:
+        o = Oracle(*(int(x) for x in tag.split("x")))
+        for s, b, d in zip(g["init_seeds_" + tag][::4], g["init_boards_" + tag][::4], g["init_draws_" + tag][::4]):
+            bb, dd = o.init_board(int(s))
+            assert (bb == b).all() and dd == d, (tag, int(s))
+        for b, lb in zip(g["legal_boards_" + tag], g["legal_" + tag]):
+            bits = np.zeros(o.A, np.uint8)
+            bits[o.legal_actions(b.astype(np.int32))] = 1
+            assert (bits == lb).all(), tag
+        if "step_board_" + tag not in g.files:
+            continue
+        cols = [g["step_" + k + "_" + tag] for k in ("board", "seed", "n_actions", "action", "next", "reward", "draws")]
+        for b, s, na, a, nx, r, d in zip(*cols):
+            if d == -2:  # the reference hangs (cycling shuffle)
+                continue
+            nb, rr, dd, f = o.apply_action(b.astype(np.int32), int(s), int(a), int(na))
+            assert (nb == nx).all() and rr == r, tag
+            if d >= 0:
+                assert dd == d, tag
+        for i, s in enumerate(g["ep_seeds_" + tag][:16]):
+            e = o.random_episode(int(s))
+            assert (e["actions"] == g["ep_actions_" + tag][i]).all(), tag
+            assert (e["rewards"] == g["ep_rewards_" + tag][i]).all(), tag
+            assert (e["final"] == g["ep_final_" + tag][i]).all(), tag

@@ -53,7 +53,7 @@ int main(int argc, char** argv) {
   for (int i = 0; i < nb; ++i) {
     seeds[i] = 1000 + i;
     FullMT* fm = new FullMT; fm->init(seeds[i], 0);
-    init_board<CF>(&boards[i * CF::NP], *fm); delete fm;
+    { NoStore ns; init_board<CF>(&boards[i * CF::NP], *fm, ns); } delete fm;
     Bd HL, VL; legal_masks<CF>(&boards[i * CF::NP], special_mask<CF, CF::NP>(&boards[i * CF::NP]), HL, VL);
     uint32_t act[CF::AW]; action_bits<CF>(HL, VL, act);
     ChainMT r; r.init(seeds[i], mt_state397(seeds[i]));
@@ -114,10 +114,10 @@ PATCHES = [  # (anchor, text inserted after it)
     ("    while (cand.any()) {                                       // row-major scan over run starts", "\n        SIM_TRIP(1);"),
     ("    while (trig.any()) {\n        const int x = trig.lowest();", "\n        SIM_TRIP(2);"),
     ("    for (;;) {  // drop every tile that has a hole somewhere below it by one row", "\n        SIM_TRIP(3);"),
-    ("    // wave would wait for its unluckiest lane on every tile.\n    for (;;) {", "\n        SIM_TRIP(4);"),
+    ("        uint32_t v = rng.next32() & tmask;", "\n        SIM_TRIP(4);"),
     ("        for (int gi = 0; gi < ng; ++gi) {                      // get_match_spawn_mask (:159-169)", "\n            SIM_TRIP(5);"),
     ("                    if ((st.get_v(gi) & rh).any()) { g = gi; break; }", "\n                    SIM_TRIP(6);"),
-    ("                if (it == limit) return CAS_PAUSED;             // paused before iteration limit + 1\n                ++it;",
+    ("                ++it;",
      "\n                SIM_ITER();\n                SIM_HOLES(VALID.andnot(tb_nonzero<CF>(P) | special_mask<CF, 6>(P)).popc());"),
 ]
 
