@@ -94,8 +94,10 @@ int ensure_host(m3_ctx* c, size_t bytes) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->hbuf) HIP_TRY(hipHostFree(c->hbuf));
     c->hbuf = nullptr;
+    c->hdev = nullptr;
     c->hcap = 0;
-    HIP_TRY(hipHostMalloc(&c->hbuf, bytes, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&c->hbuf, bytes, hipHostMallocMapped | hipHostMallocPortable));
+    HIP_TRY(hipHostGetDevicePointer(&c->hdev, c->hbuf, 0));  // the device's address of the same bytes
     c->hcap = bytes;
     return M3_OK;
 }
@@ -141,10 +143,15 @@ int stage_download(m3_ctx* c, const Image& out, std::initializer_list<void*> dst
     return M3_OK;
 }
 
-int bad_cells_error(uint32_t waves) {
-    return set_err(M3_ERR_INVALID, "cell value outside [0, 127] in %u wave(s) of 64 boards (outputs undefined)",
-                   waves);
+int bad_cells_error() {
+    return set_err(M3_ERR_INVALID, "cell value outside [0, 127] in the boards (outputs undefined)");
 }
+
+// Zero-copy path of the small host-buffer calls (the facade's batch-1 calls): the kernels read
+// the inputs from and write the outputs to the context's pinned buffer (host memory the device
+// maps), so a call is its launches and one sync, with no copy in either direction.
+constexpr int64_t ZC_MAX_BOARDS = 256;
+constexpr int ZC_OVF_WORD = 8;  // c->counters[8]: the zero-copy overflow count, kept zero between calls
 
 
 
@@ -260,6 +267,7 @@ int m3_ctx_create(int device, int rows, int columns, int types, m3_ctx** out) {
     c->sdesc = make_shape(rows, columns, types);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->counters, 256);
+    if (e == hipSuccess) e = hipMemset(c->counters, 0, 256);  // (the zero-copy overflow word starts at zero)
     if (e != hipSuccess) {
         delete c;
         return set_err(M3_ERR_HIP, "context setup: %s", hipGetErrorString(e));
@@ -318,6 +326,30 @@ int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boar
     CHECK_ARG(c && n >= 0 && (n == 0 || (seeds && out_boards)), "bad arguments");
     if (n == 0) return M3_OK;
     HIP_TRY(hipSetDevice(c->device));
+    if (n <= ZC_MAX_BOARDS) {  // zero-copy: the reset launch(es) and one sync
+        Image im;
+        const int i_s = im.add(n * 4ull), o_b = im.add(n * (size_t)c->N), o_d = im.add(n * 4ull),
+                  o_f = im.add(n * 4ull);
+        int rc = ensure_host(c, im.total + 256);
+        if (rc) return rc;
+        char* h = (char*)c->hbuf;
+        char* d = (char*)c->hdev;
+        memcpy(h + im.off[i_s], seeds, n * 4);
+        InitArgs a{};
+        a.shape = c->sdesc;
+        a.n = n;
+        a.seeds = (const uint32_t*)(d + im.off[i_s]);
+        a.boards = (int8_t*)(d + im.off[o_b]);
+        a.draws = (uint32_t*)(d + im.off[o_d]);
+        a.first_action = (int32_t*)(d + im.off[o_f]);
+        rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, n); });
+        if (rc) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        memcpy(out_boards, h + im.off[o_b], n * (size_t)c->N);
+        if (out_draws) memcpy(out_draws, h + im.off[o_d], n * 4);
+        if (out_first_action) memcpy(out_first_action, h + im.off[o_f], n * 4);
+        return M3_OK;
+    }
     Image in, out;
     in.add(n * 4ull);
     const int o_b = out.add(n * (size_t)c->N), o_d = out.add(n * 4ull), o_f = out.add(n * 4ull);
@@ -350,6 +382,52 @@ int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t*
     if (rc0) return rc0;
     HIP_TRY(hipSetDevice(c->device));
     const size_t bytes = n * (size_t)c->N;
+    if (n <= ZC_MAX_BOARDS) {  // zero-copy: two launches and one sync
+        Image im;
+        const int i_b = im.add(bytes), i_s = im.add(n * 4ull), i_na = im.add(n * 4ull), i_a = im.add(n * 4ull);
+        const int o_bad = im.add(16), o_b = im.add(bytes), o_r = im.add(n * 4ull), o_d = im.add(n * 4ull),
+                  o_f = im.add(n * 4ull), o_l = im.add(out_legal_bits ? n * 4ull * c->AW : 0),
+                  o_x = im.add(out_next_action ? n * 4ull : 0);
+        int rc = ensure_host(c, im.total + 256);
+        if (rc) return rc;
+        rc = ensure_scratch(c, n * 4ull + 256);
+        if (rc) return rc;
+        char* h = (char*)c->hbuf;  // host view
+        char* d = (char*)c->hdev;  // device view of the same pinned bytes
+        memcpy(h + im.off[i_b], boards, bytes);
+        memcpy(h + im.off[i_s], seeds, n * 4);
+        memcpy(h + im.off[i_na], n_actions, n * 4);
+        memcpy(h + im.off[i_a], actions, n * 4);
+        memset(h + im.off[o_bad], 0, 16);
+        ApplyArgs a{};
+        a.shape = c->sdesc;
+        a.n = n;
+        a.boards = (const int8_t*)(d + im.off[i_b]);
+        a.seeds = (const uint32_t*)(d + im.off[i_s]);
+        a.n_actions = (const int32_t*)(d + im.off[i_na]);
+        a.actions = (const int32_t*)(d + im.off[i_a]);
+        a.out_boards = (int8_t*)(d + im.off[o_b]);
+        a.reward = (int32_t*)(d + im.off[o_r]);
+        a.draws = (uint32_t*)(d + im.off[o_d]);
+        a.flags = (uint32_t*)(d + im.off[o_f]);
+        a.legal = out_legal_bits ? (uint32_t*)(d + im.off[o_l]) : nullptr;
+        a.next_action = out_next_action ? (int32_t*)(d + im.off[o_x]) : nullptr;
+        a.ovf_count = c->counters + ZC_OVF_WORD;
+        a.bad_cells = (uint32_t*)(d + im.off[o_bad]);
+        a.ovf_list = (uint32_t*)c->dbuf;
+        a.clear_ovf = 1;
+        rc = with_shape(c->shape, [&](auto cf) { return launch_apply<decltype(cf)>(c, a); });
+        if (rc) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (*(volatile uint32_t*)(h + im.off[o_bad])) return bad_cells_error();
+        memcpy(out_boards, h + im.off[o_b], bytes);
+        memcpy(out_reward, h + im.off[o_r], n * 4);
+        memcpy(out_draws, h + im.off[o_d], n * 4);
+        memcpy(out_flags, h + im.off[o_f], n * 4);
+        if (out_legal_bits) memcpy(out_legal_bits, h + im.off[o_l], n * 4ull * c->AW);
+        if (out_next_action) memcpy(out_next_action, h + im.off[o_x], n * 4);
+        return M3_OK;
+    }
     Image in, out;  // cell values are checked on the device while the boards are staged (k_apply)
     const int i_b = in.add(bytes), i_s = in.add(n * 4ull), i_na = in.add(n * 4ull), i_a = in.add(n * 4ull);
     const int o_cnt = out.add(16), o_b = out.add(bytes), o_r = out.add(n * 4ull), o_d = out.add(n * 4ull),
@@ -384,7 +462,7 @@ int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t*
     rc = stage_download(c, out, {cnt, out_boards, out_reward, out_draws, out_flags, out_legal_bits,
                                  out_next_action}, dout);
     if (rc) return rc;
-    return cnt[1] ? bad_cells_error(cnt[1]) : M3_OK;
+    return cnt[1] ? bad_cells_error() : M3_OK;
 }
 
 int m3_legal_actions(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* out_legal_bits) {
@@ -394,6 +472,22 @@ int m3_legal_actions(m3_ctx* c, int64_t n, const int8_t* boards, uint32_t* out_l
     int rc0 = check_ids_on_board(c);
     if (rc0) return rc0;
     HIP_TRY(hipSetDevice(c->device));
+    if (n <= ZC_MAX_BOARDS) {  // zero-copy: one launch and one sync
+        Image im;
+        const int i_b = im.add(n * (size_t)c->N), o_l = im.add(n * 4ull * c->AW);
+        int rc = ensure_host(c, im.total + 256);
+        if (rc) return rc;
+        char* h = (char*)c->hbuf;
+        char* d = (char*)c->hdev;
+        memcpy(h + im.off[i_b], boards, n * (size_t)c->N);
+        rc = with_shape(c->shape, [&](auto cf) {
+            return launch_legal<decltype(cf)>(c, n, (const int8_t*)(d + im.off[i_b]), (uint32_t*)(d + im.off[o_l]));
+        });
+        if (rc) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        memcpy(out_legal_bits, h + im.off[o_l], n * 4ull * c->AW);
+        return M3_OK;
+    }
     Image in, out;
     in.add(n * (size_t)c->N);
     out.add(n * 4ull * c->AW);
@@ -516,7 +610,7 @@ int m3_rollouts(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seed
     uint32_t cnt[4];
     rc = stage_download(c, out, {cnt, out_gain, out_steps, out_draws, out_flags, out_boards}, dout);
     if (rc) return rc;
-    return cnt[2] ? bad_cells_error(cnt[2]) : M3_OK;
+    return cnt[2] ? bad_cells_error() : M3_OK;
 }
 
 // ---- env ------------------------------------------------------------------
@@ -571,6 +665,8 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         if constexpr (K::CASCADE_LIMIT >= 0) alloc(&e->cont, RW * n * 4ull);
         return 0;
     });
+    // word 0 of every continuation record starts CONT_EMPTY (a record is ready once it holds a board index)
+    if (err == hipSuccess && e->cont) err = hipMemset(e->cont, 0xFF, n * 4ull);
     for (hipEvent_t& ev : e->gev)
         if (err == hipSuccess) err = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     // every per-board field starts zeroed: a never-reset env reads back zeros, not stale device memory

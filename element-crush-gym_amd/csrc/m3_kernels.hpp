@@ -64,6 +64,11 @@ constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 #define M3_RESET_KCAP 454
 #endif
 constexpr uint32_t RESET_KCAP = M3_RESET_KCAP;
+// 16x16x8 resets: 1 = lane-per-board on the two-block register chain (k_init_chain2),
+// 0 = lane-per-board FullMT in scratch (k_init_fix_lane)
+#ifndef M3_RESET16_CHAIN2
+#define M3_RESET16_CHAIN2 0
+#endif
 // A reset stops after this many rounds of BoardV2.__init__'s redraw loop (boardv2.py:23-27) and
 // flags M3_FLAG_RESET_CAP: only two-colour boards get near it (a 16x16x2 reset can need more than
 // 10,000 rounds; the reference keeps going), and a GPU lane must end.
@@ -96,7 +101,15 @@ struct KS {
 #define M3_CONT_WPS M3_STEP_WPS
 #endif
     static constexpr int CONT_WPS = CF::N > 128 ? 1 : M3_CONT_WPS;
+    // 1: k_env_step waves that finish their own boards take paused steps from the shard's queue
+    // (work-stealing tail, k_env_step phase 2); k_env_cont then only finishes the dead boards
+#ifndef M3_FUSED_CONT
+#define M3_FUSED_CONT 1
+#endif
     // k_env_cont's persistent waves per shard launch (each loops over the paused-step queue)
+#ifndef M3_CONT_PERSIST
+#define M3_CONT_PERSIST 0
+#endif
 #ifndef M3_CONT_WAVES
 #define M3_CONT_WAVES 1024
 #endif
@@ -324,9 +337,10 @@ __device__ __forceinline__ bool block_copy_in_checked(const int8_t* __restrict__
     return (hi & 0x80808080u) != 0u;
 }
 
-// count the waves that saw a bad cell (one atomic per such wave)
-__device__ __forceinline__ void flag_bad_cells(bool bad, uint32_t* counter) {
-    if (counter && __any((int)bad) && __lane_id() == 0) atomicAdd(counter, 1u);
+// mark that some wave saw a bad cell: a plain store of 1 (the flag may live in host memory on the
+// zero-copy path of small host-buffer calls, where device atomics are not an option)
+__device__ __forceinline__ void flag_bad_cells(bool bad, uint32_t* flag) {
+    if (flag && __any((int)bad) && __lane_id() == 0) *(volatile uint32_t*)flag = 1u;
 }
 
 template <int BLOCK>
@@ -460,7 +474,8 @@ struct ApplyArgs {
     int32_t* next_action;  // nullable
     uint32_t* ovf_count;
     uint32_t* ovf_list;
-    uint32_t* bad_cells;   // nullable: waves that saw a cell value outside [0, 127]
+    uint32_t* bad_cells;   // nullable: set to 1 if a cell value lies outside [0, 127]
+    int clear_ovf;         // k_apply_fix (one block) zeroes *ovf_count when done (zero-copy calls)
 };
 }  // namespace m3k
 using m3k::ApplyArgs;
@@ -526,7 +541,7 @@ template <class CF>
 __global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
     const uint32_t cnt = *a.ovf_count;
     const typename CF::Dim dm(a.shape);
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
+    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * FIX_BLOCK) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.boards + b * dm.cells(), P, dm);
@@ -536,6 +551,10 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
         ArrayStore<CF> st;
         apply_and_emit<CF>(P, a, b, mt, st, dm);
         planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.out_boards + b * dm.cells()), dm);
+    }
+    if (a.clear_ovf) {  // a one-block launch: every thread has read the count
+        __syncthreads();
+        if (threadIdx.x == 0) *a.ovf_count = 0u;
     }
 }
 
@@ -971,6 +990,35 @@ __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
     }
 }
 
+// One round of randint(1, T+1, (R, C)) for a power-of-two T (every draw is a
+// tile) as a rolled loop over the board's words: the RNG code appears once in
+// the kernel instead of once per unrolled word (fill_round), which keeps a
+// large generator such as ChainMT2 from multiplying the register peak.
+template <class CF, class RNG>
+__device__ __forceinline__ void fill_round_seq(typename CF::Bd* P, RNG& mt, const typename CF::Bd* only) {
+    static_assert(CF::TILE_RNG != 0u && CF::TILE_RNG == CF::TILE_MASK && CF::N % 32 == 0, "N draws per round");
+    constexpr int BITS = CF::BITS;
+#pragma unroll 1
+    for (int w = 0; w < CF::W; ++w) {
+        uint32_t t[BITS];
+#pragma unroll
+        for (int p = 0; p < BITS; ++p) t[p] = 0u;
+#pragma unroll 1
+        for (int bit = 0; bit < 32; ++bit) {
+            const uint32_t v = (mt.next32() & CF::TILE_MASK) + 1u;
+#pragma unroll
+            for (int p = 0; p < BITS; ++p) t[p] |= ((v >> p) & 1u) << bit;
+        }
+        const uint32_t m = only ? only->word_at(w) : 0xFFFFFFFFu;
+#pragma unroll
+        for (int p = 0; p < BITS; ++p) {
+#pragma unroll
+            for (int i = 0; i < CF::W; ++i)
+                if (i == w) P[p].w[i] = (P[p].w[i] & ~m) | (t[p] & m);
+        }
+    }
+}
+
 // ---- lane-per-board reset on the two-block register chain (16x16x8) -------
 // Every reset of the launch, one board per lane, on ChainMT2: the first 1248
 // raw outputs of seed(s) from registers (m3_rng.hpp), so no reset walks a
@@ -979,17 +1027,15 @@ __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
 // the lanes of a wave draw in lockstep and the chain's level changes are
 // wave-uniform. A reset that would need a round past draw 1248 (16x16x8: a
 // 5th round, ~2 % of resets) leaves the lane: appended to the defer list for
-// k_init_coop (env prefetch), or redone by its own wave at once (wave_reset)
-// when the launch has no list. stats[1] counts the resets the wave-cooperative
-// pass finishes.
+// k_init_coop (one wave per board; every launch of this kernel carries a defer
+// list). stats[1] counts the resets the wave-cooperative pass finishes.
 template <class CF>
 __global__ void __launch_bounds__(INIT_BLOCK) k_init_chain2(InitArgs a) {
-    static_assert(!CF::DYN && INIT_BLOCK == 64, "specialised shapes, one-wave blocks (wave_reset)");
+    static_assert(!CF::DYN && INIT_BLOCK == 64, "specialised shapes, one-wave blocks");
     constexpr bool LOCKSTEP = CF::TILE_RNG != 0u && CF::TILE_RNG == CF::TILE_MASK;  // N draws per round
+    static_assert(LOCKSTEP, "power-of-two tile counts (16x16x8)");
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
     if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], (uint32_t)cnt);
-    __shared__ uint32_t key_s[624];
-    __shared__ __attribute__((aligned(16))) uint8_t cell_s[(CF::N + 3) / 4 * 4 + 16];
     const typename CF::Dim dm{};
     for (int64_t base = (int64_t)blockIdx.x * INIT_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_BLOCK) {
         const int64_t i = base + threadIdx.x;
@@ -1004,18 +1050,14 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init_chain2(InitArgs a) {
             typename CF::Bd P[CF::NP], mask;
 #pragma unroll
             for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
-            fill_round<CF>(P, mt, nullptr);                                     // boardv2.py:21
+            fill_round_seq<CF>(P, mt, nullptr);                                 // boardv2.py:21
             for (;;) {                                                          // :23-27
-                if (mt.overflow) {
-                    ok = false;
-                    break;
-                }
                 if (!get_match_mask<CF>(P, mask)) break;
-                if (LOCKSTEP && mt.k + (uint32_t)CF::N > ChainMT2::LIMIT) {  // the next round leaves the chain
+                if (mt.k + (uint32_t)CF::N > ChainMT2::LIMIT) {  // the next round leaves the chain
                     ok = false;
                     break;
                 }
-                fill_round<CF>(P, mt, &mask);
+                fill_round_seq<CF>(P, mt, &mask);
             }
             if (ok) {
                 if (a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;
@@ -1024,21 +1066,13 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init_chain2(InitArgs a) {
                 init_store_board<CF>(a, ob, P, dm);
             }
         }
-        uint64_t bad = __ballot(!ok);
-        if (!bad) continue;
-        if (a.defer) {  // left to k_init_coop: one wave-aggregated append
+        const uint64_t bad = __ballot(!ok);
+        if (bad) {  // left to k_init_coop (one wave per board): one wave-aggregated append
             const int lane = (int)threadIdx.x;
             uint32_t q = 0;
             if (lane == 0) q = atomicAdd(a.defer_count, (uint32_t)__popcll(bad));
             q = __shfl(q, 0);
             if (!ok) a.defer[q + (uint32_t)__popcll(bad & ((1ull << lane) - 1ull))] = (uint32_t)i;
-            continue;
-        }
-        if (a.stats && threadIdx.x == 0) atomicAdd(&a.stats[1], (uint32_t)__popcll(bad));
-        while (bad) {
-            const int l = __builtin_ctzll(bad);
-            bad &= bad - 1ull;
-            wave_reset<CF>(a, __shfl(i, l), key_s, cell_s, (int)threadIdx.x);
         }
     }
 }
@@ -1106,7 +1140,7 @@ struct EnvArgs {
     int32_t* packed;  // nullable: reward<<2 | trunc<<1 | done for the RCCL gather
     uint32_t* counters;  // this step's block: [0] overflow count, [1] prefetch count, [2] prefetch overflow
                          // count, [3] spill records used, [4] continuation records, [5] records taken
-                         // by k_env_cont
+                         // (k_env_step phase 2 / persistent k_env_cont), [6] dead-board records
     uint32_t* spill;     // group-table spill pool of the shard
     uint32_t* stats;     // [0] step recomputes
     uint32_t* ovf_list;
@@ -1253,6 +1287,86 @@ __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a
 template <class CF>
 using EnvCont = Cont<CF, typename KS<CF>::Rng>;
 
+// ---- work-stealing continuation (M3_FUSED_CONT) --------------------------
+// Record q of the queue is written as: every state word, then -- once the
+// writing wave's board stores are out -- (release) its board index in word 0,
+// so a wave taking q waits until word 0 is not CONT_EMPTY. Word 0 of every record is CONT_EMPTY between steps: the taker
+// (or k_env_cont, for the dead queue) restores it after reading.
+constexpr uint32_t CONT_EMPTY = 0xFFFFFFFFu;
+
+template <class CF, class RNG>
+__device__ __forceinline__ void cont_write(uint32_t* rec, int64_t cs, const typename CF::Bd* P, const RNG& rng, int r,
+                                           uint32_t f) {
+    Cont<CF, RNG>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
+}
+
+// a settled board with no legal move: the dead queue, from the top of the record area down
+template <class CF>
+__device__ __forceinline__ void cont_dead(const EnvArgs& a, int64_t b, const typename CF::Bd* P,
+                                          const typename KS<CF>::Rng& rng, int r, uint32_t f) {
+    const uint32_t qd = atomicAdd(&a.counters[6], 1u);
+    uint32_t* rec = a.cont + (a.n - 1 - (int64_t)qd);
+    cont_write<CF>(rec, a.cont_stride, P, rng, r, f | FLAG_CONT_DEAD);
+    rec[0] = (uint32_t)b;
+}
+
+// Phase 2 of k_env_step: take up to 64 queued records at a time (never past the
+// count reserved so far, so a record taken is one some running wave is writing)
+// and run each to its end -- the cascade unbounded, a board that settles dead
+// to the dead queue. A wave leaves when the queue is empty; a wave still in
+// phase 1 that queues more records comes here afterwards and takes them.
+template <class CF, class Store>
+__device__ __forceinline__ void env_steal(const EnvArgs& a, Store& st, const typename CF::Dim& dm) {
+    using K = KS<CF>;
+    const int t = threadIdx.x;
+    for (;;) {
+        uint32_t base = 0u, k = 0u;
+        if (t == 0) {
+            for (;;) {
+                const uint32_t T = __hip_atomic_load(&a.counters[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t R = __hip_atomic_load(&a.counters[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (T >= R) break;
+                const uint32_t want = R - T < 64u ? R - T : 64u;
+                if (atomicCAS(&a.counters[5], T, T + want) == T) {
+                    base = T;
+                    k = want;
+                    break;
+                }
+            }
+        }
+        base = __shfl(base, 0);
+        k = __shfl(k, 0);
+        if (k == 0u) break;
+        if ((uint32_t)t < k) {
+            uint32_t* rec = a.cont + base + t;
+            uint32_t bw;
+            while ((bw = __hip_atomic_load(rec, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == CONT_EMPTY)
+                __builtin_amdgcn_s_sleep(2);
+            const int64_t b = bw;
+            const int64_t cs = a.cont_stride;
+            typename CF::Bd P[CF::NP], HL, VL;
+            typename K::Rng rng;
+            int r;
+            uint32_t f;
+            EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
+            rec[0] = CONT_EMPTY;
+            const int mv = a.moves[b], sc0 = a.score[b];
+            const int c = apply_cascade_ex<CF, CASX_STOP_DEAD>(P, rng, f, HL, VL, st, r, -1, false, dm);
+            if (c == CAS_DEAD && !(f & FLAG_RECOMPUTE)) {
+                cont_dead<CF>(a, b, P, rng, r, f);
+            } else {
+                const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm);
+                if (!ok) {
+                    const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+                    a.ovf_list[slot] = (uint32_t)b;
+                } else {
+                    planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
+                }
+            }
+        }
+    }
+}
+
 template <class CF>
 __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArgs a) {
     // The board staging area is only live before the cascade (HBM -> LDS ->
@@ -1287,6 +1401,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     st.spill = a.spill;
     st.pool_next = &a.counters[3];
     st.pool_cap = K::SPILL_RECORDS;
+    uint32_t pub_q = ~0u, pub_b = 0u;  // this lane's queued record (M3_FUSED_CONT), marked ready at the end
     if (t < nb) {
         const int64_t b = b0 + t;
         typename CF::Bd P[CF::NP];
@@ -1307,18 +1422,40 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
         }
         // paused steps leave a continuation record (one atomic per wave)
         const bool paused = res == ENV_STEP_PAUSED;
-        const uint64_t m = K::CASCADE_LIMIT >= 0 ? __ballot(paused) : 0ull;
-        if (m) {
-            const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            if (paused) {
-                const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                uint32_t* rec = a.cont + q;
-                const int64_t cs = a.cont_stride;
-                rec[0] = (uint32_t)b;
-                EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
+        if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT) {
+            // cascades past the bound join the shard's queue (phase 2 below takes them); boards that
+            // settled dead go to the dead queue at the top of the record area (k_env_cont, after).
+            // A queued record is only marked ready after this wave's board stores below: its board
+            // slot in nxt holds stale bytes until the record's taker writes the finished board.
+            const bool dead = paused && (f & FLAG_CONT_DEAD);
+            const bool cont = paused && !dead;
+            const uint64_t m = __ballot(cont);
+            if (m) {
+                const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
+                base = __shfl(base, leader);
+                if (cont) {
+                    pub_q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                    pub_b = (uint32_t)b;
+                    cont_write<CF>(a.cont + pub_q, a.cont_stride, P, rng, r, f);
+                }
+            }
+            if (dead) cont_dead<CF>(a, b, P, rng, r, f);
+        } else {
+            const uint64_t m = K::CASCADE_LIMIT >= 0 ? __ballot(paused) : 0ull;
+            if (m) {
+                const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
+                base = __shfl(base, leader);
+                if (paused) {
+                    const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                    uint32_t* rec = a.cont + q;
+                    const int64_t cs = a.cont_stride;
+                    rec[0] = (uint32_t)b;
+                    EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
+                }
             }
         }
         planes_to_bytes<CF>(P, lds + t * NC, dm);  // a paused board's bytes are rewritten by k_env_cont
@@ -1337,6 +1474,14 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     }
     lds_sync();
     block_copy_out<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
+    if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT) {
+        if (pub_q != ~0u) {  // the board stores above are visible before the record is marked ready
+            __threadfence();
+            __hip_atomic_store(a.cont + pub_q, pub_b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        lds_sync();  // the group table reuses the staging area
+        env_steal<CF>(a, st, dm);
+    }
 #ifdef M3_PHASE_PROF
     if (live) st.end(0);
 #endif
@@ -1406,13 +1551,53 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont(EnvArg
                     const uint32_t slot = atomicAdd(&a.counters[0], 1u);
                     a.ovf_list[slot] = (uint32_t)b;
                 } else {
-                    constexpr int NW = (CF::N + 3) / 4;
-                    uint32_t cw[NW];
-                    words_from_planes<CF>(P, cw);
-                    store_cells<CF::N>(reinterpret_cast<uint8_t*>(a.nxt + b * CF::N), cw);
+                    planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
                 }
                 b = -1;
             }
+        }
+    }
+}
+
+// (M3_CONT_PERSIST=0) One paused step per lane, each run to its end.
+// Finish the steps k_env_step paused (their cascade ran past KS::CASCADE_LIMIT
+// inner iterations): the long cascades of a launch, packed densely into waves
+// instead of holding every lane of their k_env_step wave idle. Grid-stride
+// over the records; each board is written straight to nxt.
+template <class CF>
+__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont_grid(EnvArgs a) {
+    using K = KS<CF>;
+    // The few waves of this kernel are the step's critical path; they share SIMDs with
+    // the other shard's step waves and the resets: issue first (A/B: within noise).
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
+    const uint32_t cnt = M3_FUSED_CONT ? a.counters[6] : a.counters[4];  // (fused: the dead queue only)
+    LdsStore<CF, K::GCAP, K::B> st{as_lds(tab + threadIdx.x)};
+    st.spill = a.spill;
+    st.pool_next = &a.counters[3];
+    st.pool_cap = K::SPILL_RECORDS;
+    const int64_t cs = a.cont_stride;
+    for (uint32_t q = blockIdx.x * K::B + threadIdx.x; q < cnt; q += gridDim.x * K::B) {
+        uint32_t* rec = a.cont + (M3_FUSED_CONT ? a.n - 1 - (int64_t)q : (int64_t)q);
+        const int64_t b = rec[0];
+        if (M3_FUSED_CONT) rec[0] = CONT_EMPTY;
+        typename CF::Bd P[CF::NP];
+        typename K::Rng rng;
+        int r;
+        uint32_t f;
+        EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
+        const int mv = a.moves[b], sc0 = a.score[b];
+        typename CF::Bd HL, VL;
+        const bool dead = (f & FLAG_CONT_DEAD) != 0;  // settled with no legal move: continue at the shuffle
+        f &= ~FLAG_CONT_DEAD;
+        const typename CF::Dim dm(a.shape);
+        apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, -1, dead, dm);
+        const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm);
+        if (!ok) {
+            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+            a.ovf_list[slot] = (uint32_t)b;
+        } else {
+            planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
         }
     }
 }
@@ -1422,7 +1607,7 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
     const uint32_t cnt = a.counters[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], cnt);
     const typename CF::Dim dm(a.shape);
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
+    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * FIX_BLOCK) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.cur + b * dm.cells(), P, dm);
@@ -1572,7 +1757,7 @@ template <class CF>
 __global__ void __launch_bounds__(FIX_BLOCK) k_rollout_fix(RolloutArgs a) {
     const uint32_t cnt = a.counters[0];
     const typename CF::Dim dm(a.shape);
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += FIX_GRID * FIX_BLOCK) {
+    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * FIX_BLOCK) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.boards + b * dm.cells(), P, dm);
@@ -1628,6 +1813,7 @@ struct m3_ctx {
     // pinned host staging of the host-buffer calls: inputs go up as one image, outputs come back
     // as one image (one copy each way per call, include/m3.h "stateless batch calls")
     void* hbuf = nullptr;
+    void* hdev = nullptr;  // hbuf as the device addresses it (zero-copy calls)
     size_t hcap = 0;
     uint32_t* counters = nullptr;  // rollouts: [0] overflow count, [1] spill records, [2] bad-cell waves
 };
@@ -1723,7 +1909,7 @@ int launch_apply(m3_ctx* c, const ApplyArgs& a) {
     if (a.n == 0) return M3_OK;  // (*a.ovf_count and *a.bad_cells are zero: the caller's upload)
     hipLaunchKernelGGL(k_apply<CF>, dim3(grid_for<CF>(a.n)), dim3(KS<CF>::B), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_apply_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
+    hipLaunchKernelGGL(k_apply_fix<CF>, dim3(a.clear_ovf ? 1 : FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }
@@ -1741,7 +1927,7 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
             gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
             hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
         }
-    } else if constexpr (!CF::DYN) {  // 16x16x8: ~60 % of resets need the second MT block
+    } else if constexpr (!CF::DYN && M3_RESET16_CHAIN2) {  // 16x16x8: ~60 % of resets need the second MT block
         hipLaunchKernelGGL(k_init_chain2<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
         if (a.defer) {  // the ~2 % past draw 1248, one wave per board
             HIP_TRY(hipGetLastError());
@@ -1843,10 +2029,19 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
     HIP_TRY(hipGetLastError());
     if constexpr (KS<CF>::CASCADE_LIMIT >= 0) {
+#if M3_CONT_PERSIST
         // persistent waves over the device-side queue of paused steps (~19 % of the boards at limit 2)
         int64_t g = ((int64_t)(sh.n * 0.2) + KS<CF>::B - 1) / KS<CF>::B;
         g = g < 1 ? 1 : (g > M3_CONT_WAVES ? M3_CONT_WAVES : g);
         hipLaunchKernelGGL(k_env_cont<CF>, dim3((unsigned)g), dim3(KS<CF>::B), 0, st, a);
+#elif M3_FUSED_CONT
+        // the dead boards left by k_env_step's phases (~1e-5 of the steps): a few blocks, grid-strided
+        hipLaunchKernelGGL(k_env_cont_grid<CF>, dim3(FIX_GRID), dim3(KS<CF>::B), 0, st, a);
+#else
+        // grid-strides over the device-side count of paused steps: sized for their usual share (~20 % at limit 2)
+        const int64_t g = ((int64_t)(sh.n * 0.25) + KS<CF>::B - 1) / KS<CF>::B;
+        hipLaunchKernelGGL(k_env_cont_grid<CF>, dim3((unsigned)(g > 0 ? g : 1)), dim3(KS<CF>::B), 0, st, a);
+#endif
         HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
@@ -1869,7 +2064,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.list_slot = e->pf_slot[par] + o;
         r.list_count = &cnt[1];
         r.stats = base + 41;
-        if constexpr (!CF::DYN) {
+        if constexpr (INIT_INLINE_FIX<CF> || (!CF::DYN && M3_RESET16_CHAIN2)) {
             r.defer = e->defer + o;
             r.defer_count = &cnt[2];  // zeroed with the block
         }

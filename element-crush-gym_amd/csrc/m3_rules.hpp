@@ -719,11 +719,46 @@ M3_HD int get_matches(const typename CF::Bd* P, typename CF::Bd& mask, typename 
     return match_scan<CF, true>(P, mask, sw, st);
 }
 
-// mask only (BoardV2.__init__ only asks "any match?" and which cells)
+// mask only (BoardV2.__init__ only asks "any match?" and which cells,
+// boardv2.py:23-27), by the sequential scan
 template <class CF>
-M3_HD bool get_match_mask(const typename CF::Bd* P, typename CF::Bd& mask) {
+M3_HD bool get_match_mask_scan(const typename CF::Bd* P, typename CF::Bd& mask) {
     NoStore ns;
     return match_scan<CF, false>(P, mask, nullptr, ns) != MATCH_NONE;
+}
+
+// The same mask without the per-start loop whenever that is provably equal.
+// The scan visits each maximal run's first start (leftmost / top cell) unless
+// an EARLIER run already covers it: an h-run start inside a v-run from above,
+// or a v-run start inside an h-run from its left (the dropped-arm quirk). If no
+// start cell is covered by a run of the other direction that began before it,
+// every maximal run is added whole and the mask is just the union of all runs
+// of three or more; otherwise fall back to the scan. Uniform cost, a handful of
+// whole-board operations (no loop over run starts).
+template <class CF>
+M3_HD bool get_match_mask(const typename CF::Bd* P, typename CF::Bd& mask) {
+    using Bd = typename CF::Bd;
+    using G = typename CF::G;
+    constexpr int C = CF::C, R = CF::R;
+    constexpr Bd CLE2 = G::col_le(C - 2), RLE2 = G::row_le(R - 2);
+    const Bd nz = tb_nonzero<CF>(P);
+    const Bd e1h = CLE2 & tb_eq<CF, 1>(P);
+    const Bd e1v = RLE2 & tb_eq<CF, C>(P);
+    const Bd h3 = nz & e1h & at<1>(e1h);        // a horizontal triple starts here
+    const Bd v3 = nz & e1v & at<C>(e1v);        // a vertical triple starts here
+    if (!(h3 | v3).any()) {
+        mask = Bd::zero();
+        return false;
+    }
+    const Bd hc = h3 | at<-1>(h3) | at<-2>(h3);             // every cell of a horizontal run
+    const Bd vc = v3 | at<-C>(v3) | at<-2 * C>(v3);         // every cell of a vertical run
+    const Bd hin = hc.andnot(h3.andnot(at<-1>(h3)));        // run cells right of the run's first start
+    const Bd vin = vc.andnot(v3.andnot(at<-C>(v3)));        // run cells below the run's top
+    if (!((h3 & vin) | (v3 & hin)).any()) {
+        mask = hc | vc;
+        return true;
+    }
+    return get_match_mask_scan<CF>(P, mask);
 }
 
 // --------------------------------------------------------------------------

@@ -378,6 +378,24 @@ long hc_paused(int reset) {
     if (reset) g_paused = 0;
     return v;
 }
+// boards whose match mask differs between the fast path and the sequential scan
+long hc_mask_mismatches(int cfg, long n, const int8_t* b) {
+    long bad = 0;
+#define CALL(CF)                                                                   \
+    for (long i = 0; i < n; ++i) {                                                 \
+        typename CF::Bd P[CF::NP], m1, m2;                                         \
+        const typename CF::Dim dm_ = make_dim<CF>();                               \
+        load_planes<CF>(b + i * dm_.cells(), P, dm_);                              \
+        const bool a1 = get_match_mask<CF>(P, m1);                                 \
+        const bool a2 = get_match_mask_scan<CF>(P, m2);                            \
+        bool same = a1 == a2;                                                      \
+        for (int w = 0; w < CF::W; ++w) same = same && m1.w[w] == m2.w[w];         \
+        bad += !same;                                                              \
+    }
+    DISPATCH(cfg, CALL);
+#undef CALL
+    return bad;
+}
 // first n raw outputs via ChainMT2 (the two-block register chain); -1 once it overflowed
 int hc_chain2_raw(uint32_t seed, int n, uint32_t* out) {
     ChainMT2 g;

@@ -31,6 +31,8 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         _lib.hc_chain_draw.restype = ctypes.c_uint32
         _lib.hc_chain_draw.argtypes = [ctypes.c_uint32, ctypes.c_int]
+        _lib.hc_mask_mismatches.restype = ctypes.c_long
+        _lib.hc_mask_mismatches.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_void_p]
     return _lib
 
 
@@ -67,6 +69,13 @@ class HostCore:
         self.recomputed = lib().hc_apply(self.cfg, ctypes.c_long(n), _p(boards), _p(seeds), _p(na), _p(acts),
                                          _p(out), _p(rew), _p(drw), _p(flg), _p(legal), _p(nxt), int(small))
         return out, rew, drw, flg, legal, nxt
+
+    def mask_mismatches(self, boards):
+        """boards whose fast match mask (union of runs when no run start is covered by an earlier
+        run of the other direction) differs from the sequential scan's"""
+        boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
+        self._sel()
+        return lib().hc_mask_mismatches(self.cfg, ctypes.c_long(len(boards)), _p(boards))
 
     def init(self, seeds):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint32)

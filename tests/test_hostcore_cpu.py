@@ -37,6 +37,19 @@ def test_chain2_equals_numpy_stream_over_two_blocks():
         assert lib().hc_chain2_raw(ctypes.c_uint32(s), 1249, got.ctypes.data_as(ctypes.c_void_p)) == -1
 
 
+@pytest.mark.parametrize("shape", [(9, 9, 6), (16, 16, 8), (7, 7, 3), (9, 9, 2), (12, 5, 4)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_fast_match_mask_equals_scan(shape):
+    """BoardV2.__init__'s match mask (boardv2.py:23-27) by the union-of-runs fast path equals the
+    sequential get_matches scan on dense random boards (few types: many L / T / crossing runs,
+    so the dropped-arm fallback is exercised too), the mask of the reset and its fixtures."""
+    R, C, T = shape
+    hc = HostCore(R, C, T)
+    rng = np.random.default_rng(7)
+    b = rng.integers(1, T + 1, size=(20000, R * C)).astype(np.int8)
+    assert hc.mask_mismatches(b) == 0
+
+
 @pytest.mark.parametrize("tag", list(SHAPES))
 def test_roundtrip_planes(tag):
     hc = HostCore(*SHAPES[tag])

@@ -10,7 +10,7 @@ O=gpurun_out/$TAG
 mkdir -p $O/s9 $O/s16
 S16="--shape 16x16x8 --boards 262144"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
-{ timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ]; } && \
+{ timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ]; } && \
 timeout -k 10 300 python3 bench.py > $O/s9/bench.log 2>&1 && \
 timeout -k 10 300 python3 bench.py $S16 --steps 40 --warmup 10 > $O/s16/bench.log 2>&1 && \
 timeout -k 10 300 python3 bench.py --rollouts --steps 5 --warmup 1 > $O/rollouts9.log 2>&1 && \

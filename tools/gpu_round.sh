@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 B="bench.py --steps 30 --warmup 5 --no-cpu-baseline $XB"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
-{ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ]; } && \
+{ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ]; } && \
 timeout -k 10 300 python bench.py --steps 60 --warmup 10 --cpu-seconds 8 $XB > $OUT/bench.log 2>&1 && \
 timeout -k 10 300 python bench.py --shape 16x16x8 --boards 262144 --steps 40 --warmup 10 --cpu-seconds 8 > $OUT/bench16.log 2>&1 && \
 timeout -k 10 300 python bench.py --rollouts --steps 5 --warmup 1 > $OUT/rollouts9.log 2>&1 && \
