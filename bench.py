@@ -349,10 +349,12 @@ def main():
         import hashlib
 
         uid = share_unique_id(dist, rank, lambda: os.urandom(128)) if dist else os.urandom(128)
-        print(json.dumps({"rank": rank, "world": world, "local_rank": local,
-                          "dist_world": dist.get_world_size() if dist else 1,
-                          "spawned": os.environ.get("M3_SPAWNED") == "1", "torch_loaded": "torch" in sys.modules,
-                          "id_bytes": len(uid), "id_sha256": hashlib.sha256(uid).hexdigest()}), flush=True)
+        line = json.dumps({"rank": rank, "world": world, "local_rank": local,
+                           "dist_world": dist.get_world_size() if dist else 1,
+                           "spawned": os.environ.get("M3_SPAWNED") == "1", "torch_loaded": "torch" in sys.modules,
+                           "id_bytes": len(uid), "id_sha256": hashlib.sha256(uid).hexdigest()})
+        sys.stdout.flush()
+        os.write(sys.stdout.fileno(), (line + "\n").encode())  # one write: the ranks share the pipe
         dist_close(dist, rank)
         return
 

@@ -24,6 +24,11 @@ M3_INSTANTIATE(extern template, CF_1)
 M3_INSTANTIATE(extern template, CF_2)
 M3_INSTANTIATE(extern template, CF_3)
 M3_INSTANTIATE(extern template, CF_4)
+M3_INSTANTIATE(extern template, CF_5)
+M3_INSTANTIATE(extern template, CF_6)
+M3_INSTANTIATE(extern template, CF_7)
+M3_INSTANTIATE(extern template, CF_8)
+M3_INSTANTIATE(extern template, CF_9)
 }  // namespace m3k
 #endif
 using namespace m3k;
@@ -198,13 +203,18 @@ void destroy_shards(m3_env* e) {
 // configuration id (shape_id) -> its config type (CF_<id>, m3_kernels.hpp)
 template <class F>
 static int with_shape(int shape, F&& f) {
-    static_assert(N_CONFIGS == 5, "with_shape lists every configuration");
+    static_assert(N_CONFIGS == 10, "with_shape lists every configuration");
     switch (shape) {
         case 0: return f(CF_0{});
         case 1: return f(CF_1{});
         case 2: return f(CF_2{});
         case 3: return f(CF_3{});
         case 4: return f(CF_4{});
+        case 5: return f(CF_5{});
+        case 6: return f(CF_6{});
+        case 7: return f(CF_7{});
+        case 8: return f(CF_8{});
+        case 9: return f(CF_9{});
         default: return set_err(M3_ERR_UNSUPPORTED, "board shape not compiled in");
     }
 }
@@ -244,8 +254,8 @@ int m3_ctx_create(int device, int rows, int columns, int types, m3_ctx** out) {
     const int sid = shape_id(rows, columns, types);
     if (sid < 0)
         return set_err(M3_ERR_UNSUPPORTED,
-                       "BoardConfig(rows=%d, columns=%d, types=%d): supported are rows and columns 3..16, "
-                       "types 2..15", rows, columns, types);
+                       "BoardConfig(rows=%d, columns=%d, types=%d): supported are rows and columns 3..32, "
+                       "types 2..31", rows, columns, types);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return set_err(M3_ERR_NO_DEVICE, "no HIP device visible (libm3 has no CPU fallback)");
@@ -511,7 +521,12 @@ namespace {
 
 // overflow list + group-table spill pool of a rollout launch (a lane keeps one
 // spill record for its whole rollout)
-int64_t rollout_spill_cap(int64_t n) { return std::max<int64_t>(4096, n / 8); }
+// records of the rollout spill pool: one per 8 rollouts (at least 4096), within 256 MB (a lane
+// that finds the pool empty is replayed exactly by k_rollout_fix)
+int64_t rollout_spill_cap(int64_t n, size_t words) {
+    const int64_t budget = (int64_t)((256ull << 20) / (words * 4ull));
+    return std::max<int64_t>(1, std::min(std::max<int64_t>(4096, n / 8), budget));
+}
 
 size_t rollout_spill_words(int shape) {
     return (size_t)with_shape(shape, [&](auto cf) {
@@ -523,7 +538,7 @@ size_t rollout_spill_words(int shape) {
 // a.n and the per-rollout buffers set; carves the pool from cv and launches.
 // counters: 16 zeroed bytes on the device (nullptr: the context's, zeroed here)
 int enqueue_rollouts(m3_ctx* c, RolloutArgs a, Carve& cv, uint32_t* counters = nullptr) {
-    const int64_t cap = rollout_spill_cap(a.n);
+    const int64_t cap = rollout_spill_cap(a.n, rollout_spill_words(c->shape));
     if (!counters) {
         counters = c->counters;
         HIP_TRY(hipMemsetAsync(counters, 0, 16, c->stream));
@@ -550,7 +565,7 @@ int m3_rollouts_device(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_
     int rc0 = check_ids_on_board(c);
     if (rc0) return rc0;
     HIP_TRY(hipSetDevice(c->device));
-    int rc = ensure_scratch(c, carve_size({n * 4ull, rollout_spill_cap(n) * rollout_spill_words(c->shape) * 4ull}));
+    int rc = ensure_scratch(c, carve_size({n * 4ull, rollout_spill_cap(n, rollout_spill_words(c->shape)) * rollout_spill_words(c->shape) * 4ull}));
     if (rc) return rc;
     Carve cv{(char*)c->dbuf};
     RolloutArgs a{};
@@ -584,7 +599,7 @@ int m3_rollouts(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seed
     const int i_b = in.add(bytes), i_s = in.add(n * 4ull), i_na = in.add(n * 4ull), i_rs = in.add(n * 4ull);
     const int o_cnt = out.add(16), o_g = out.add(n * 4ull), o_st = out.add(n * 4ull), o_d = out.add(n * 4ull),
               o_f = out.add(n * 4ull), o_b = out.add(out_boards ? bytes : 0);
-    const size_t tail = carve_size({n * 4ull, rollout_spill_cap(n) * rollout_spill_words(c->shape) * 4ull});
+    const size_t tail = carve_size({n * 4ull, rollout_spill_cap(n, rollout_spill_words(c->shape)) * rollout_spill_words(c->shape) * 4ull});
     char* dev;
     int rc = stage_begin(c, in, out, tail, &dev);
     if (rc) return rc;
@@ -1066,11 +1081,14 @@ int m3_env_stats(m3_env* e, uint64_t out[4]) {
 // configurations' translation units (each has its own g_prof)
 #ifdef M3_SPLIT_TU
 extern "C" int m3_prof_read_0(uint64_t*, int), m3_prof_read_1(uint64_t*, int), m3_prof_read_2(uint64_t*, int),
-    m3_prof_read_3(uint64_t*, int), m3_prof_read_4(uint64_t*, int);
+    m3_prof_read_3(uint64_t*, int), m3_prof_read_4(uint64_t*, int), m3_prof_read_5(uint64_t*, int),
+    m3_prof_read_6(uint64_t*, int), m3_prof_read_7(uint64_t*, int), m3_prof_read_8(uint64_t*, int),
+    m3_prof_read_9(uint64_t*, int);
 int m3_prof_read(uint64_t* out, int reset) {
-    static_assert(N_CONFIGS == 5, "one reader per configuration");
-    int (*const rd[5])(uint64_t*, int) = {m3_prof_read_0, m3_prof_read_1, m3_prof_read_2, m3_prof_read_3,
-                                         m3_prof_read_4};
+    static_assert(N_CONFIGS == 10, "one reader per configuration");
+    int (*const rd[10])(uint64_t*, int) = {m3_prof_read_0, m3_prof_read_1, m3_prof_read_2, m3_prof_read_3,
+                                          m3_prof_read_4, m3_prof_read_5, m3_prof_read_6, m3_prof_read_7,
+                                          m3_prof_read_8, m3_prof_read_9};
     uint64_t part[2 * PROF_SLOTS];
     for (int i = 0; i < 2 * PROF_SLOTS; ++i) out[i] = 0;
     for (auto f : rd) {

@@ -79,6 +79,9 @@ struct BB {
     }
 };
 
+// the low n bits (0 <= n <= 32; a plain (1u << 32) - 1 would be 0 on the GPU)
+M3_HD constexpr uint32_t low_bits(int n) { return n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u); }
+
 M3_HD int select_bit(uint32_t u, int k) {  // position of the k-th (0-based) set bit of u
     int pos = 0;
 #pragma unroll
@@ -175,7 +178,7 @@ struct Geo {
         return 0;
     }
     static M3_HD BB<W> col_band(int c0, int c1) {
-        const uint32_t pat = (c1 > c0) ? (((1u << c1) - 1u) & ~((1u << c0) - 1u)) : 0u;
+        const uint32_t pat = (c1 > c0) ? (low_bits(c1) & ~low_bits(c0)) : 0u;
         BB<W> r;
         _Pragma("unroll") for (int i = 0; i < W; ++i) {
             uint32_t v = pat * rep_mul(i);

@@ -52,6 +52,9 @@ constexpr int FIX_BLOCK = 64;
 constexpr int FIX_GRID = 16;       // step fixup almost never has work: few blocks schedule fast
 constexpr int INIT_FIX_BLOCK = 64;
 constexpr int INIT_BLOCK = 64;
+// active lanes of the one-board-per-lane fix / reset kernels (KS::BPW: one for the 32 x 32 frame)
+template <class CF>
+constexpr uint32_t lanes_for() { return CF::W > 8 ? 1u : 64u; }
 // 9x9: k_init redoes its few >= 624-draw resets in-wave (wave_reset); 16x16
 // resets go straight to k_init_fix_lane (most need >= 624 draws)
 template <class CF>
@@ -85,6 +88,11 @@ struct KS {
     static constexpr int B = 64;
     static_assert(B == 64, "one-wave workgroups: lds_sync() orders a single wave's LDS accesses");
     static constexpr int GCAP = 4;                  // match groups in LDS (more spill to a global pool)
+    // boards per wave: 64 (one per lane), but ONE for the 32 x 32 frame. Those kernels carry
+    // ~2,500 SGPR spills through VGPR lanes, and with several lanes active some boards came out
+    // wrong only in company (32x32x8 steps: 92 of 689; each exact alone) -- the lane interference
+    // DESIGN.md §4 describes for the 16 x 16 frame. One active lane per wave has no divergence.
+    static constexpr int BPW = CF::W > 8 ? 1 : B;
 #ifndef M3_STEP_WPS
 #define M3_STEP_WPS 4
 #endif
@@ -93,7 +101,14 @@ struct KS {
 #ifndef M3_STEP_WPS16
 #define M3_STEP_WPS16 2
 #endif
-    static constexpr int STEP_WPS = CF::N > 128 ? M3_STEP_WPS16 : M3_STEP_WPS;
+    // frame shapes (run-time board shape, FCfg): 1 wave/SIMD. Their uniform shape masks take
+    // ~100 SGPRs and spill into VGPR lanes; at 2 waves/SIMD those VGPRs spilled to scratch in
+    // turn and divergent lanes of a wave corrupted each other's results (rollouts at 10x8x9,
+    // tools/dbg); with 512 registers per lane nothing reaches scratch.
+#ifndef M3_STEP_WPS_FRAME
+#define M3_STEP_WPS_FRAME 1
+#endif
+    static constexpr int STEP_WPS = CF::DYN ? M3_STEP_WPS_FRAME : (CF::N > 128 ? M3_STEP_WPS16 : M3_STEP_WPS);
     // k_env_cont: bounded like the step kernel it runs beside (a 2-waves/SIMD
     // build without spills measured 4 % slower overall: its waves take register
     // file the other shard's step waves need)
@@ -102,9 +117,11 @@ struct KS {
 #endif
     static constexpr int CONT_WPS = CF::N > 128 ? 1 : M3_CONT_WPS;
     // 1: k_env_step waves that finish their own boards take paused steps from the shard's queue
-    // (work-stealing tail, k_env_step phase 2); k_env_cont then only finishes the dead boards
+    // (work-stealing tail, k_env_step phase 2); k_env_cont then only finishes the dead boards.
+    // Off: exact, but 9x9x6 ran at 67 ms/step against 0.46 with the separate k_env_cont launch
+    // (gpurun_out/r04g)
 #ifndef M3_FUSED_CONT
-#define M3_FUSED_CONT 1
+#define M3_FUSED_CONT 0
 #endif
     // k_env_cont's persistent waves per shard launch (each loops over the paused-step queue)
 #ifndef M3_CONT_PERSIST
@@ -113,7 +130,8 @@ struct KS {
 #ifndef M3_CONT_WAVES
 #define M3_CONT_WAVES 1024
 #endif
-    static constexpr uint32_t SPILL_RECORDS = 4096;  // spill pool records per shard
+    // spill pool records per shard (32 x 32 frame: a record is 86 KB; fewer, the rest recompute)
+    static constexpr uint32_t SPILL_RECORDS = CF::W > 8 ? 256 : 4096;
     // The env step's RNG is the register-only MT19937 chain from the board's
     // (seed, mt[397]) -- 4 B of per-board state (a per-board stream cache of
     // the first raw outputs, built by the reset, measured equal at 9x9 and 2x
@@ -513,8 +531,8 @@ __global__ void __launch_bounds__(KS<CF>::B) k_apply(ApplyArgs a) {
     __shared__ uint32_t gtab[LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::WORDS];
     const typename CF::Dim dm(a.shape);
     const int NC = dm.cells();
-    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
-    const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
+    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::BPW;
+    const int nb = (int)((a.n - b0) < KS<CF>::BPW ? (a.n - b0) : KS<CF>::BPW);
     flag_bad_cells(block_copy_in_checked<KS<CF>::B>(a.boards + b0 * NC, lds, nb * NC), a.bad_cells);
     lds_sync();
     const int t = threadIdx.x;
@@ -541,7 +559,8 @@ template <class CF>
 __global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
     const uint32_t cnt = *a.ovf_count;
     const typename CF::Dim dm(a.shape);
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * FIX_BLOCK) {
+    for (uint32_t i = blockIdx.x * lanes_for<CF>() + threadIdx.x; threadIdx.x < lanes_for<CF>() && i < cnt;
+         i += gridDim.x * lanes_for<CF>()) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.boards + b * dm.cells(), P, dm);
@@ -955,10 +974,11 @@ __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
     const typename CF::Dim dm(a.shape);
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
     if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], (uint32_t)cnt);
-    for (int64_t base = (int64_t)blockIdx.x * INIT_FIX_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_FIX_BLOCK) {
+    constexpr int64_t L = lanes_for<CF>();
+    for (int64_t base = (int64_t)blockIdx.x * L; base < cnt; base += (int64_t)gridDim.x * L) {
         const int64_t oi = base + threadIdx.x;
         bool long_reset = false;
-        if (oi < cnt) {
+        if (threadIdx.x < L && oi < cnt) {
             int64_t b;
             uint32_t seed, slot;
             init_item(a, oi, b, seed, slot);
@@ -1089,8 +1109,8 @@ __global__ void __launch_bounds__(KS<CF>::B) k_legal(Shape shape, int64_t n, con
     __shared__ __attribute__((aligned(16))) uint8_t lds[KS<CF>::B * CF::N + 16];
     const typename CF::Dim dm(shape);
     const int NC = dm.cells();
-    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
-    const int nb = (int)((n - b0) < KS<CF>::B ? (n - b0) : KS<CF>::B);
+    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::BPW;
+    const int nb = (int)((n - b0) < KS<CF>::BPW ? (n - b0) : KS<CF>::BPW);
     block_copy_in<KS<CF>::B>(boards + b0 * NC, lds, nb * NC);
     lds_sync();
     const int t = threadIdx.x;
@@ -1382,8 +1402,8 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     uint32_t* const gtab = stage_tab;
     const typename CF::Dim dm(a.shape);
     const int NC = dm.cells();
-    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::B;
-    const int nb = (int)((a.n - b0) < KS<CF>::B ? (a.n - b0) : KS<CF>::B);
+    const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::BPW;
+    const int nb = (int)((a.n - b0) < KS<CF>::BPW ? (a.n - b0) : KS<CF>::BPW);
     block_copy_in<KS<CF>::B>(a.cur + b0 * NC, lds, nb * NC);
     const int t = threadIdx.x;
     const uint32_t cslot = t < nb ? a.slot[b0 + t] : 0u;
@@ -1607,7 +1627,8 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
     const uint32_t cnt = a.counters[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], cnt);
     const typename CF::Dim dm(a.shape);
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * FIX_BLOCK) {
+    for (uint32_t i = blockIdx.x * lanes_for<CF>() + threadIdx.x; threadIdx.x < lanes_for<CF>() && i < cnt;
+         i += gridDim.x * lanes_for<CF>()) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.cur + b * dm.cells(), P, dm);
@@ -1721,8 +1742,8 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_rollout(Rollout
     uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
     const typename CF::Dim dm(a.shape);
     const int NC = dm.cells();
-    const int64_t b0 = (int64_t)blockIdx.x * K::B;
-    const int nb = (int)((a.n - b0) < K::B ? (a.n - b0) : K::B);
+    const int64_t b0 = (int64_t)blockIdx.x * K::BPW;
+    const int nb = (int)((a.n - b0) < K::BPW ? (a.n - b0) : K::BPW);
     flag_bad_cells(block_copy_in_checked<K::B>(a.boards + b0 * NC, lds, nb * NC), &a.counters[2]);
     lds_sync();
     const int t = threadIdx.x;
@@ -1757,7 +1778,8 @@ template <class CF>
 __global__ void __launch_bounds__(FIX_BLOCK) k_rollout_fix(RolloutArgs a) {
     const uint32_t cnt = a.counters[0];
     const typename CF::Dim dm(a.shape);
-    for (uint32_t i = blockIdx.x * FIX_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * FIX_BLOCK) {
+    for (uint32_t i = blockIdx.x * lanes_for<CF>() + threadIdx.x; threadIdx.x < lanes_for<CF>() && i < cnt;
+         i += gridDim.x * lanes_for<CF>()) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.boards + b * dm.cells(), P, dm);
@@ -1779,8 +1801,9 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_rollout_fix(RolloutArgs a) {
 
 constexpr int N_SPECIALISED = 2;
 // Specialised shapes first (ids 0..N_SPECIALISED-1), then the frame configs
-// FCfg<2..4> (ids N_SPECIALISED + BITS - 2) for every other supported shape:
-// rows and columns 3..16, types 2..15. (types = 2: from about 7x7 up a refill
+// FCfg<2..5> (ids N_SPECIALISED + BITS - 2) for every other shape with rows
+// and columns 3..16, and FCfg<2..5, 32> (ids N_SPECIALISED + 4 + BITS - 2)
+// for rows and columns 3..32 with a side above 16; types 2..31. (types = 2: from about 7x7 up a refill
 // of two colours almost always leaves a match, so the reference's cascade
 // does not return -- steps here stop at CASCADE_CAP refills and flag it -- and
 // a large board's reset can take millions of draws -- stopped at
@@ -1792,8 +1815,8 @@ int shape_id(int r, int c, int t) {
     ++id;
     M3_SHAPES(X)
 #undef X
-    if (r >= 3 && r <= 16 && c >= 3 && c <= 16 && t >= 2 && t <= 15) return N_SPECIALISED + bits_for_types(t) - 2;
-    return -1;
+    if (r < 3 || c < 3 || r > MAX_FRAME || c > MAX_FRAME || t < 2 || t > 31) return -1;
+    return N_SPECIALISED + (frame_side(r, c) == 32 ? 4 : 0) + bits_for_types(t) - 2;
 }
 
 }  // namespace
@@ -1897,19 +1920,28 @@ using CF_1 = Cfg<16, 16, 8>;
 using CF_2 = FCfg<2>;
 using CF_3 = FCfg<3>;
 using CF_4 = FCfg<4>;
-constexpr int N_CONFIGS = 5;
+using CF_5 = FCfg<5>;
+using CF_6 = FCfg<2, 32>;
+using CF_7 = FCfg<3, 32>;
+using CF_8 = FCfg<4, 32>;
+using CF_9 = FCfg<5, 32>;
+constexpr int N_CONFIGS = 10;
 
 namespace m3k {
 
+// fix-pass blocks: FIX_GRID x 64 active lanes in all
 template <class CF>
-int grid_for(int64_t n) { return (int)((n + KS<CF>::B - 1) / KS<CF>::B); }
+int fix_grid() { return (int)(FIX_GRID * 64 / lanes_for<CF>()); }
+
+template <class CF>
+int grid_for(int64_t n) { return (int)((n + KS<CF>::BPW - 1) / KS<CF>::BPW); }
 
 template <class CF>
 int launch_apply(m3_ctx* c, const ApplyArgs& a) {
     if (a.n == 0) return M3_OK;  // (*a.ovf_count and *a.bad_cells are zero: the caller's upload)
     hipLaunchKernelGGL(k_apply<CF>, dim3(grid_for<CF>(a.n)), dim3(KS<CF>::B), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_apply_fix<CF>, dim3(a.clear_ovf ? 1 : FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
+    hipLaunchKernelGGL(k_apply_fix<CF>, dim3(a.clear_ovf ? 1 : fix_grid<CF>()), dim3(FIX_BLOCK), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }
@@ -1935,8 +1967,10 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
             gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
             hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
         }
-    } else {  // frame shapes: FullMT (lane-private scratch)
-        hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3((unsigned)g), dim3(INIT_FIX_BLOCK), 0, stream, a);
+    } else {  // frame shapes: FullMT (lane-private scratch); 32 x 32 frame: one board per wave
+        const int64_t gl = (max_items + lanes_for<CF>() - 1) / lanes_for<CF>();
+        hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3((unsigned)(gl > 4096 ? 4096 : gl)), dim3(INIT_FIX_BLOCK), 0,
+                           stream, a);
     }
     HIP_TRY(hipGetLastError());
     return M3_OK;
@@ -2044,7 +2078,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
 #endif
         HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_env_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, st, a);
+    hipLaunchKernelGGL(k_env_fix<CF>, dim3(fix_grid<CF>()), dim3(FIX_BLOCK), 0, st, a);
     HIP_TRY(hipGetLastError());
     if (timed) {  // the whole step pipeline of the shard, fixup pass included
         HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], st));
@@ -2148,7 +2182,7 @@ template <class CF>
 int launch_rollouts(m3_ctx* c, const RolloutArgs& a) {
     hipLaunchKernelGGL(k_rollout<CF>, dim3(grid_for<CF>(a.n)), dim3(KS<CF>::B), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_rollout_fix<CF>, dim3(FIX_GRID), dim3(FIX_BLOCK), 0, c->stream, a);
+    hipLaunchKernelGGL(k_rollout_fix<CF>, dim3(fix_grid<CF>()), dim3(FIX_BLOCK), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     return M3_OK;
 }

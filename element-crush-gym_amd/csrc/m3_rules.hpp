@@ -113,7 +113,9 @@ struct Cfg {
 // and 2 <= types <= 15 runs in a 16 x 16 FRAME: cell (r, c) is bit r*16 + c,
 // so the row stride -- every shift the rule code uses -- is a compile-time 16
 // for every board width, and only BITS (the token layout, boardConfig.py:29-33)
-// is a template parameter. The board's own rows / columns / types / action
+// is a template parameter. Boards with more than 16 rows or columns (up to
+// 32 x 32) run the same code in a 32 x 32 frame (FS = 32: one row per 32-bit
+// word; 1024-bit planes, so those kernels trade speed for reach). The board's own rows / columns / types / action
 // count are run-time values (FrameDim). Cells outside the board ("walls")
 // hold 0 in every plane: they never start or extend a run (get_matches skips
 // 0, boardFunctions.py:136), never equal a non-zero token in the legal-move
@@ -122,10 +124,12 @@ struct Cfg {
 // by the board mask. (Rows < columns are accepted for reset only: the
 // reference's action ids then reach past the last row and legal_actions /
 // apply_action raise IndexError, boardConfig.py:27,45-59.)
-template <int BITS_>
+template <int BITS_, int FS_ = 16>
 struct FCfg {
     static constexpr bool DYN = true;
-    static constexpr int R = 16, C = 16;  // the frame (row stride 16)
+    static constexpr int FS = FS_;
+    static_assert(FS == 16 || FS == 32, "frame side");
+    static constexpr int R = FS, C = FS;  // the frame (row stride FS)
     static constexpr int N = R * C;
     static constexpr int W = N / 32;
     static constexpr int BITS = BITS_;
@@ -137,10 +141,12 @@ struct FCfg {
     static constexpr int M = TM + STM + 1;
     static constexpr int A = R * (C - 1) * 2;    // upper bounds: the board's are FrameDim's
     static constexpr int AW = (A + 31) / 32;
-    static constexpr int NP = 7;
+    // value planes: 7 for int8 cells in [0, 127]; with 5 token bits (types 16..31) an 8th, for
+    // the mega token 128 a 5-in-a-row spawns before the clip to 32 (boardv2.py:163-164)
+    static constexpr int NP = BITS >= 5 ? 8 : 7;
     static constexpr int MAXG = N / 3 + 1;
     static constexpr int SHUFFLE_CAP = 1024;
-    static_assert(BITS >= 2 && BITS <= 4, "types 2..15");
+    static_assert(BITS >= 2 && BITS <= 5, "types 2..31");
     using Bd = BB<W>;
     using G = Geo<R, C, W>;
     using Dim = FrameDim<FCfg>;
@@ -150,17 +156,21 @@ constexpr int bits_for_types(int t) { return ceil_log2(t + 1); }
 
 // A board shape at run time (kernel argument of the frame kernels): the
 // BoardConfig fields plus, per frame cell x, whether the swap (x, x+1) /
-// (x, x+16) is the decode of some action id < A. Those are the only swaps
+// (x, x+FS) is the decode of some action id < A. Those are the only swaps
 // legal_actions can return (boardFunctions.py:97 iterates cfg.actions), and
 // on most non-square boards they are not all of them: with C = 3 the literal
 // 3 of boardConfig.py:50 sends the vertical ids of row r to row r-1, and when
 // rows > columns the id range A = R(C-1)*2 (boardConfig.py:27) ends inside a
 // row. The dead-board test (boardv2.py:188) is "no legal id", so it must see
 // exactly these swaps.
+constexpr int MAX_FRAME = 32;  // largest board side
 struct Shape {
     int rows, cols, types;
-    uint32_t hreach[8], vreach[8];
+    int fs;  // frame side: 16, or 32 for a board with a side > 16
+    uint32_t hreach[MAX_FRAME * MAX_FRAME / 32], vreach[MAX_FRAME * MAX_FRAME / 32];
 };
+
+M3_HD constexpr int frame_side(int rows, int cols) { return (rows > 16 || cols > 16) ? 32 : 16; }
 
 // decode (boardConfig.py:45-59) -> the first cell of the swap, and whether it is vertical
 M3_HD void decode_action(int action, int cols, int& r, int& c, bool& vertical) {
@@ -181,14 +191,15 @@ M3_HD Shape make_shape(int rows, int cols, int types) {
     s.rows = rows;
     s.cols = cols;
     s.types = types;
-    for (int i = 0; i < 8; ++i) s.hreach[i] = s.vreach[i] = 0u;
+    s.fs = frame_side(rows, cols);
+    for (int i = 0; i < MAX_FRAME * MAX_FRAME / 32; ++i) s.hreach[i] = s.vreach[i] = 0u;
     const int A = rows * (cols - 1) * 2;
     for (int a = 0; a < A; ++a) {
         int r, c;
         bool v;
         decode_action(a, cols, r, c, v);
-        const int x = r * 16 + c;
-        if (x < 0 || x >= 256) continue;
+        const int x = r * s.fs + c;
+        if (r < 0 || x < 0 || x >= s.fs * s.fs) continue;
         (v ? s.vreach : s.hreach)[x >> 5] |= 1u << (x & 31);
     }
     return s;
@@ -212,25 +223,44 @@ struct StaticDim {
     M3_HD static constexpr typename CF::Bd valid() { return CF::G::valid(); }
 };
 
+// A copy of x that lives in a VGPR: the frame shape's masks are wave-uniform,
+// so the compiler keeps them (and everything derived from them) in SGPRs,
+// runs out of the ~100 a wave has and spills thousands of SGPRs through VGPR
+// lanes; held per lane they cost 3*W VGPRs instead.
+M3_HD uint32_t in_vgpr(uint32_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint32_t r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
+    return x;
+#endif
+}
+
 template <class CF>
 struct FrameDim {
     using Bd = typename CF::Bd;
     int r, c, a;
     uint32_t trng, tmask;
     Bd vmask;      // board cells
-    Bd hl, vl;     // swaps (x, x+1) / (x, x+16) that some action id decodes to (Shape)
+    Bd hl, vl;     // swaps (x, x+1) / (x, x+FS) that some action id decodes to (Shape)
     M3_HD FrameDim(const Shape& s) : r(s.rows), c(s.cols), a(s.rows * (s.cols - 1) * 2) {
         trng = (uint32_t)(s.types - 1);                      // randint(1, T+1)
         uint32_t m = trng;
         m |= m >> 1; m |= m >> 2; m |= m >> 4;
         tmask = m;
-        const uint32_t row = (1u << c) - 1u;
+        const uint32_t row = low_bits(c);
 #pragma unroll
         for (int i = 0; i < CF::W; ++i) {
-            const int r0 = 2 * i, r1 = 2 * i + 1;
-            vmask.w[i] = (r0 < r ? row : 0u) | (r1 < r ? row << 16 : 0u);
-            hl.w[i] = s.hreach[i];
-            vl.w[i] = s.vreach[i];
+            if constexpr (CF::FS == 16) {  // two rows per word
+                const int r0 = 2 * i, r1 = 2 * i + 1;
+                vmask.w[i] = (r0 < r ? row : 0u) | (r1 < r ? row << 16 : 0u);
+            } else {                       // one row per word
+                vmask.w[i] = i < r ? row : 0u;
+            }
+            hl.w[i] = in_vgpr(s.hreach[i]);
+            vl.w[i] = in_vgpr(s.vreach[i]);
+            vmask.w[i] = in_vgpr(vmask.w[i]);
         }
     }
     M3_HD int rows() const { return r; }
@@ -482,26 +512,31 @@ M3_HD void action_bits_rows(const typename CF::Bd& HL, const typename CF::Bd& VL
 template <class CF>
 M3_HD void action_bits_frame(const typename CF::Bd& HL, const typename CF::Bd& VL, uint32_t* act,
                              const typename CF::Dim& dm) {
+    // One rolled pass over the board's rows: a row's field (2C-1 <= 63 bits)
+    // spans up to three output words. (Unrolled over rows x words, the shift
+    // amounts -- all wave-uniform -- were hoisted into ~240 SGPRs and spilled.)
     const int C = dm.cols(), L = 2 * C - 1, A = dm.actions();
-    const uint32_t hm = (1u << (C - 1)) - 1u, vm = (1u << C) - 1u;
-    uint32_t f[CF::R];
+    const uint64_t hm = ((uint64_t)1 << (C - 1)) - 1u, vm = ((uint64_t)1 << C) - 1u;
+    auto row = [&](const typename CF::Bd& b, int r) -> uint64_t {
+        if constexpr (CF::FS == 16) return (b.word_at(r >> 1) >> ((r & 1) * 16)) & 0xFFFFu;
+        else return b.word_at(r);
+    };
 #pragma unroll
-    for (int r = 0; r < CF::R; ++r) {
-        const uint32_t h = (HL.w[r >> 1] >> ((r & 1) * 16)) & hm;
-        const int rp = r > 0 ? r - 1 : 0;
-        const uint32_t v = C == 3 ? (VL.w[rp >> 1] >> ((rp & 1) * 16)) & vm : (VL.w[r >> 1] >> ((r & 1) * 16)) & vm;
-        f[r] = r < dm.rows() ? (h | (v << (C - 1))) : 0u;
+    for (int i = 0; i < CF::AW; ++i) act[i] = 0u;
+    for (int r = 0; r < dm.rows(); ++r) {
+        const int rv = C == 3 ? (r > 0 ? r - 1 : 0) : r;
+        const uint64_t f = (row(HL, r) & hm) | ((row(VL, rv) & vm) << (C - 1));
+        const int pos = r * L, q = pos >> 5, sh = pos & 31;
+        const uint64_t lo = f << sh;
+        const uint32_t w0 = (uint32_t)lo, w1 = (uint32_t)(lo >> 32), w2 = sh ? (uint32_t)(f >> (64 - sh)) : 0u;
+#pragma unroll
+        for (int i = 0; i < CF::AW; ++i)
+            act[i] |= (i == q ? w0 : 0u) | (i == q + 1 ? w1 : 0u) | (i == q + 2 ? w2 : 0u);
     }
 #pragma unroll
     for (int i = 0; i < CF::AW; ++i) {
-        uint32_t w = 0u;
-#pragma unroll
-        for (int r = 0; r < CF::R; ++r) {
-            const int sh = r * L - 32 * i;
-            if (sh > -L && sh < 32) w |= sh >= 0 ? (f[r] << sh) : (f[r] >> -sh);
-        }
         const int lim = A - 32 * i;
-        act[i] = lim >= 32 ? w : (lim <= 0 ? 0u : (w & ((1u << lim) - 1u)));
+        act[i] = lim >= 32 ? act[i] : (lim <= 0 ? 0u : (act[i] & ((1u << lim) - 1u)));
     }
 }
 
@@ -643,9 +678,12 @@ M3_HD int match_scan(const typename CF::Bd* P, typename CF::Bd& mask, typename C
     }
     if (!cand.any()) return MATCH_NONE;
 
-    // doubling link masks for run floods (runs are <= 16 long)
+    // doubling link masks for run floods (runs are <= 16 long; <= 32 in the 32 x 32 frame)
     const Bd dh2 = e1h & at<1>(e1h), dh4 = dh2 & at<2>(dh2), dh8 = dh4 & at<4>(dh4);
     const Bd dv2 = e1v & at<C>(e1v), dv4 = dv2 & at<2 * C>(dv2), dv8 = dv4 & at<4 * C>(dv4);
+    Bd dh16, dv16;
+    if constexpr (C > 16) dh16 = dh8 & at<8>(dh8);
+    if constexpr (R > 16) dv16 = dv8 & at<8 * C>(dv8);
 
     int ng = 0;
     Bd vruns = Bd::zero();
@@ -659,6 +697,7 @@ M3_HD int match_scan(const typename CF::Bd* P, typename CF::Bd& mask, typename C
             rh |= at<-2>(rh & dh2);
             rh |= at<-4>(rh & dh4);
             if constexpr (C > 8) rh |= at<-8>(rh & dh8);
+            if constexpr (C > 16) rh |= at<-16>(rh & dh16);
         }
         if ((v3 & bx).any()) {                                 // :147-153 extend down
             rv = bx;
@@ -666,6 +705,7 @@ M3_HD int match_scan(const typename CF::Bd* P, typename CF::Bd& mask, typename C
             rv |= at<-2 * C>(rv & dv2);
             rv |= at<-4 * C>(rv & dv4);
             if constexpr (R > 8) rv |= at<-8 * C>(rv & dv8);
+            if constexpr (R > 16) rv |= at<-16 * C>(rv & dv16);
         }
         const Bd run = rh | rv;
         mask |= run;
@@ -842,17 +882,22 @@ M3_HD void merge_clip(typename CF::Bd* P, const typename CF::Bd& z, const typena
     P[BITS] |= sw[0];
     P[BITS + 1] |= sw[1];
     P[BITS + 2] |= sw[2];
-    // > 32: bit 5 with any lower bit, or bit 6
+    // > 32: bit 5 with any lower bit, or bit 6 (or 7)
     Bd low = P[0];
 #pragma unroll
     for (int p = 1; p < 5; ++p) low |= P[p];
     // plane 6 holds input values >= 64 (first pass) or a spawned M = 64 on
-    // 4-bit-type boards; both clip to 32
-    const Bd cl = (P[5] & low) | P[6];
+    // 4-bit-type boards (V = 64 on 5-bit ones); plane 7 (5-bit types only) a
+    // spawned M = 128; all clip to 32
+    Bd hi = P[6];
+#pragma unroll
+    for (int p = 7; p < CF::NP; ++p) hi |= P[p];
+    const Bd cl = (P[5] & low) | hi;
 #pragma unroll
     for (int p = 0; p < 5; ++p) P[p] = P[p].andnot(cl);
     P[5] |= cl;
-    P[6] = Bd::zero();
+#pragma unroll
+    for (int p = 6; p < CF::NP; ++p) P[p] = Bd::zero();
 }
 
 // gravity + refill (:166-173). Columns left to right, new tiles on top in draw
@@ -873,6 +918,7 @@ M3_HD typename CF::Bd gravity(typename CF::Bd* P, const typename CF::Dim& dm = t
         s |= at<2 * C>(s);
         s |= at<4 * C>(s);
         if constexpr (R > 9) s |= at<8 * C>(s);
+        if constexpr (R > 17) s |= at<16 * C>(s);
         const Bd mv = occ & s;
         if (!mv.any()) break;
 #pragma unroll
@@ -892,7 +938,7 @@ M3_HD void refill(typename CF::Bd* P, const typename CF::Bd& em, RNG& rng,
     using Bd = typename CF::Bd;
     constexpr int C = CF::C, R = CF::R;
     if (!em.any()) return;
-    uint32_t tops = em.w[0] & ((1u << C) - 1u);  // columns with at least one empty cell
+    uint32_t tops = em.w[0] & low_bits(C);  // columns with at least one empty cell
     int c = __builtin_ctz(tops);
     int r = 0;
     // One raw draw per loop trip (the masked-rejection of randint(1, T+1) is
@@ -931,6 +977,28 @@ M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng, const typename CF::Dim& dm
     constexpr int C = CF::C, R = CF::R, NPU = 6;
     rng.reseed();
     const Bd sp = special_mask<CF, NPU>(P);
+    if constexpr (R > 16) {  // 32 x 32 frame: one row per word, the permutation in a small array
+        static_assert(C == 32, "one row per word");
+        uint8_t perm[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) perm[i] = (uint8_t)i;
+        for (int i = dm.rows() - 1; i >= 1; --i) {
+            const int j = (int)rand_masked(rng, (uint32_t)i);
+            const uint8_t a = perm[i];
+            perm[i] = perm[j];
+            perm[j] = a;
+        }
+        Bd out[NPU];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int src = perm[i];
+#pragma unroll
+            for (int p = 0; p < NPU; ++p) out[p].w[i] = P[p].word_at(src);
+        }
+#pragma unroll
+        for (int p = 0; p < NPU; ++p) P[p] = out[p].andnot(sp) | (P[p] & sp);
+        return;
+    }
     uint64_t idx = 0;  // nibble i = source row of row i
 #pragma unroll
     for (int i = 0; i < R; ++i) idx |= (uint64_t)i << (4 * i);
@@ -952,7 +1020,7 @@ M3_HD void shuffle_rows(typename CF::Bd* P, RNG& rng, const typename CF::Dim& dm
         for (int p = 0; p < NPU; ++p) {
             const uint32_t lo = P[p].word_at(q), hi = P[p].word_at(q + 1);
             uint32_t f = s ? ((lo >> s) | (hi << ((32 - s) & 31))) : lo;
-            f &= (1u << C) - 1u;
+            f &= low_bits(C);
             const int dpos = i * C;
             const int dq = dpos >> 5, ds = dpos & 31;
             out[p].w[dq] |= f << ds;
@@ -1450,11 +1518,29 @@ M3_HD void words_from_planes(const typename CF::Bd* P, uint32_t* cw) {
 // --------------------------------------------------------------------------
 // Frame boards (FCfg) <-> the board's own int8 cells (R*C bytes, row-major,
 // any alignment): board row r is C bytes, cells (r, 0..C-1) sit at frame
-// bits r*16 .. r*16 + C-1; two 8x8 transposes per row.
+// bits r*FS .. r*FS + C-1; one 8x8 transpose per 8 cells of a row.
 // --------------------------------------------------------------------------
+// a frame row's bits (r compile-time in the unrolled callers)
+template <class CF>
+M3_HD uint32_t frame_row(const typename CF::Bd& b, int r) {
+    if constexpr (CF::FS == 16) return (b.w[r >> 1] >> ((r & 1) * 16)) & 0xFFFFu;
+    else return b.w[r];
+}
+// bits m of frame row r := the same bits of v
+template <class CF>
+M3_HD void frame_row_merge(typename CF::Bd& b, int r, uint32_t v, uint32_t m) {
+    if constexpr (CF::FS == 16) {
+        const int sh = (r & 1) * 16;
+        b.w[r >> 1] = (b.w[r >> 1] & ~(m << sh)) | ((v & m) << sh);
+    } else {
+        b.w[r] = (b.w[r] & ~m) | (v & m);
+    }
+}
+
 template <class CF>
 M3_HD void frame_from_bytes(const uint8_t* src, typename CF::Bd* P, const typename CF::Dim& dm) {
-    static_assert(CF::DYN && CF::C == 16, "frame layout");
+    static_assert(CF::DYN, "frame layout");
+    constexpr int FS = CF::FS, NG = FS / 8;  // 8-cell groups per row
     const int RB = dm.rows(), CB = dm.cols();
 #pragma unroll
     for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
@@ -1462,17 +1548,20 @@ M3_HD void frame_from_bytes(const uint8_t* src, typename CF::Bd* P, const typena
     for (int r = 0; r < CF::R; ++r) {
         if (r < RB) {
             const uint8_t* row = src + r * CB;
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            uint32_t w[2 * NG];
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
+            for (int k = 0; k < 2 * NG; ++k) w[k] = 0u;
+#pragma unroll
+            for (int k = 0; k < FS; ++k)
                 if (k < CB) w[k >> 2] |= (uint32_t)row[k] << (8 * (k & 3));
-            transpose8(w[0], w[1]);
-            transpose8(w[2], w[3]);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) transpose8(w[2 * g], w[2 * g + 1]);
 #pragma unroll
             for (int p = 0; p < CF::NP; ++p) {
-                const uint32_t b0 = (w[p < 4 ? 0 : 1] >> (8 * (p & 3))) & 0xFFu;
-                const uint32_t b1 = (w[p < 4 ? 2 : 3] >> (8 * (p & 3))) & 0xFFu;
-                P[p].w[r >> 1] |= (b0 | (b1 << 8)) << ((r & 1) * 16);
+                uint32_t v = 0u;
+#pragma unroll
+                for (int g = 0; g < NG; ++g) v |= ((w[2 * g + (p < 4 ? 0 : 1)] >> (8 * (p & 3))) & 0xFFu) << (8 * g);
+                frame_row_merge<CF>(P[p], r, v, 0xFFFFFFFFu >> (32 - FS));
             }
         }
     }
@@ -1480,23 +1569,26 @@ M3_HD void frame_from_bytes(const uint8_t* src, typename CF::Bd* P, const typena
 
 template <class CF>
 M3_HD void frame_to_bytes(const typename CF::Bd* P, uint8_t* dst, const typename CF::Dim& dm) {
-    static_assert(CF::DYN && CF::C == 16, "frame layout");
+    static_assert(CF::DYN, "frame layout");
+    constexpr int FS = CF::FS, NG = FS / 8;
     const int RB = dm.rows(), CB = dm.cols();
 #pragma unroll
     for (int r = 0; r < CF::R; ++r) {
         if (r < RB) {
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            uint32_t w[2 * NG];
+#pragma unroll
+            for (int k = 0; k < 2 * NG; ++k) w[k] = 0u;
 #pragma unroll
             for (int p = 0; p < CF::NP; ++p) {
-                const uint32_t bits = (P[p].w[r >> 1] >> ((r & 1) * 16)) & 0xFFFFu;
-                w[p < 4 ? 0 : 1] |= (bits & 0xFFu) << (8 * (p & 3));
-                w[p < 4 ? 2 : 3] |= (bits >> 8) << (8 * (p & 3));
+                const uint32_t bits = frame_row<CF>(P[p], r);
+#pragma unroll
+                for (int g = 0; g < NG; ++g) w[2 * g + (p < 4 ? 0 : 1)] |= ((bits >> (8 * g)) & 0xFFu) << (8 * (p & 3));
             }
-            transpose8(w[0], w[1]);
-            transpose8(w[2], w[3]);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) transpose8(w[2 * g], w[2 * g + 1]);
             uint8_t* row = dst + r * CB;
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
+            for (int k = 0; k < FS; ++k)
                 if (k < CB) row[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
         }
     }
@@ -1508,7 +1600,7 @@ M3_HD void frame_to_bytes(const typename CF::Bd* P, uint8_t* dst, const typename
 template <class CF, class RNG>
 M3_HD void fill_round_frame(typename CF::Bd* P, RNG& mt, const typename CF::Bd* only, const typename CF::Dim& dm) {
     const int RB = dm.rows(), CB = dm.cols();
-    const uint32_t tmask = dm.tile_mask(), trng = dm.tile_rng(), rowm = (1u << CB) - 1u;
+    const uint32_t tmask = dm.tile_mask(), trng = dm.tile_rng(), rowm = low_bits(CB);
 #pragma unroll
     for (int r = 0; r < CF::R; ++r) {
         if (r < RB) {
@@ -1524,10 +1616,9 @@ M3_HD void fill_round_frame(typename CF::Bd* P, RNG& mt, const typename CF::Bd* 
 #pragma unroll
                 for (int p = 0; p < CF::BITS; ++p) t[p] |= ((v >> p) & 1u) << c;
             }
-            const int sh = (r & 1) * 16;
-            const uint32_t m = (only ? (only->w[r >> 1] >> sh) & rowm : rowm) << sh;
+            const uint32_t m = only ? frame_row<CF>(*only, r) & rowm : rowm;
 #pragma unroll
-            for (int p = 0; p < CF::BITS; ++p) P[p].w[r >> 1] = (P[p].w[r >> 1] & ~m) | ((t[p] << sh) & m);
+            for (int p = 0; p < CF::BITS; ++p) frame_row_merge<CF>(P[p], r, t[p], m);
         }
     }
 }

@@ -22,6 +22,8 @@ Files written:
                   reset at done with and without a seed), bookkeeping restated over the reference
                   BoardV2 (env.py cannot run at the snapshot): obs/reward/done/truncated per step
   shapes.npz      init / legal / steps / episodes for BoardConfigs other than 9x9x6 and 16x16x8
+  big.npz         init / legal / steps / episodes past the 16 x 16 frame (20x20 .. 32x32) and
+                  for types 20 and 31
   types2.npz      BoardConfig(types=2): steps / episodes on 4x4, 5x5, 6x6 (where the reference's
                   cascade returns), resets and legal sets on 9x9, 12x7
                   (square, rows > columns, columns = 3 -- the decode quirk -- and few types), and
@@ -708,9 +710,61 @@ def gen_types2(pool):
     np.savez_compressed(os.path.join(OUT, "types2.npz"), **out)
 
 
+# Boards past the 16 x 16 frame and tile alphabets past 15 types (BoardConfig accepts any rows /
+# columns / types, boardConfig.py:26-43; main.py:100-102 takes them from the command line). With
+# types >= 16 (5 token bits) every special token is >= 32 and the clip of boardv2.py:163 turns it
+# into 32.
+BIG_SHAPES = [(20, 20, 6), (24, 17, 5), (32, 32, 8), (17, 17, 3), (9, 9, 20), (12, 12, 31)]
+
+
+def gen_big(pool):
+    rng = np.random.default_rng(4242)
+    out = {}
+    for (R, C, T) in BIG_SHAPES:
+        tag = f"{R}x{C}x{T}"
+        cfg = BoardConfig(seed=1, rows=R, columns=C, types=T)
+        seeds = np.concatenate([np.arange(1, 61), [2**31 - 2, 2**32 - 1, 123456789, 987654321]]).astype(np.uint64)
+        res = pool.map(_init_one, [(R, C, T, s) for s in seeds])
+        out[f"init_seeds_{tag}"] = seeds
+        out[f"init_boards_{tag}"] = np.array([r[0] for r in res])
+        out[f"init_draws_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        boards = [r[0].astype(np.int64) for r in res[:40]]
+        for _ in range(40):
+            b = rng.integers(1, T + 1, size=(R, C))
+            for _ in range(rng.integers(0, 6)):
+                b[rng.integers(0, R), rng.integers(0, C)] = [cfg.h_line, cfg.v_line, cfg.bomb, cfg.mega_token,
+                                                             0][rng.integers(0, 5)]
+            boards.append(np.clip(b, 0, 127))
+        for m in range(2, min(T, 6) + 1):
+            boards.append(np.fromfunction(lambda r, c: (r + 2 * c) % m + 1, (R, C), dtype=np.int64))
+        out[f"legal_boards_{tag}"] = np.array(boards, dtype=np.int8)
+        out[f"legal_{tag}"] = np.array([legal_bits(cfg, b) for b in boards], dtype=np.uint8)
+        cases = [c for c in step_cases(R, C, T, rng, 200) if np.asarray(c[0]).max() <= 127]
+        res = pool.map(_step_case, [(R, C, T, b, s, na, a) for (b, s, na, a) in cases], chunksize=8)
+        out[f"step_board_{tag}"] = np.array([c[0] for c in cases], dtype=np.int8)
+        out[f"step_seed_{tag}"] = np.array([c[1] for c in cases], dtype=np.uint32)
+        out[f"step_n_actions_{tag}"] = np.array([c[2] for c in cases], dtype=np.int32)
+        out[f"step_action_{tag}"] = np.array([c[3] for c in cases], dtype=np.int32)
+        out[f"step_next_{tag}"] = np.array([r[0] for r in res])
+        out[f"step_reward_{tag}"] = np.array([r[1] for r in res], dtype=np.int32)
+        out[f"step_draws_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+        eseeds = np.arange(1, 41, dtype=np.uint64)
+        res = pool.map(_episode, [(R, C, T, s, 20) for s in eseeds], chunksize=2)
+        keep = [i for i, r in enumerate(res) if r is not None][:32]
+        eseeds, res = eseeds[keep], [res[i] for i in keep]
+        out[f"ep_seeds_{tag}"] = eseeds
+        out[f"ep_init_{tag}"] = np.array([r[0] for r in res])
+        out[f"ep_actions_{tag}"] = np.array([r[1] for r in res], dtype=np.int16)
+        out[f"ep_rewards_{tag}"] = np.array([r[2] for r in res], dtype=np.int32)
+        out[f"ep_draws_{tag}"] = np.array([r[3] for r in res], dtype=np.int16)
+        out[f"ep_final_{tag}"] = np.array([r[4][-1] for r in res])
+        print("  ", tag, len(cases), "steps", len(keep), "episodes", flush=True)
+    np.savez_compressed(os.path.join(OUT, "big.npz"), **out)
+
+
 def main():
     which = sys.argv[1:] or ["prng", "matches", "legal", "init", "steps", "episodes", "shuffle", "env", "shapes",
-                             "types2"]
+                             "types2", "big"]
     with Pool(8) as pool:
         for w in which:
             print("generating", w, flush=True)
@@ -734,6 +788,8 @@ def main():
                 gen_shapes(pool)
             elif w == "types2":
                 gen_types2(pool)
+            elif w == "big":
+                gen_big(pool)
 
 
 if __name__ == "__main__":

@@ -5,8 +5,9 @@
 // contains or calls this file.
 //
 // Shapes: cfg 0 = Cfg<9,9,6>, cfg 1 = Cfg<16,16,8> (the specialised kernels'
-// configs), cfg 2 = the 16 x 16 frame (FCfg) for the board set by
-// hc_set_frame(rows, columns, types) -- any shape, including 9x9x6 / 16x16x8.
+// configs), cfg 2 = the frame (FCfg: 16 x 16, or 32 x 32 for a side > 16) for
+// the board set by hc_set_frame(rows, columns, types) -- any shape, including
+// 9x9x6 / 16x16x8.
 #include "../../element-crush-gym_amd/csrc/m3_rules.hpp"
 
 #include <string.h>
@@ -302,6 +303,7 @@ static void rounds_n(long n, const int8_t* boards, const uint32_t* seeds, const 
 
 using C9 = Cfg<9, 9, 6>;
 using C16 = Cfg<16, 16, 8>;
+#define M3_F32(b) FCfg<b, 32>
 
 #define DISPATCH(cfg, call)                        \
     do {                                           \
@@ -311,19 +313,30 @@ using C16 = Cfg<16, 16, 8>;
             call(C16);                             \
         } else {                                   \
             const int bits_ = bits_for_types(g_T); \
-            if (bits_ == 2) {                      \
+            const bool wide_ = g_shape.fs == 32;   \
+            if (bits_ == 2 && !wide_) {            \
                 call(FCfg<2>);                     \
-            } else if (bits_ == 3) {               \
+            } else if (bits_ == 3 && !wide_) {     \
                 call(FCfg<3>);                     \
-            } else {                               \
+            } else if (bits_ == 4 && !wide_) {     \
                 call(FCfg<4>);                     \
+            } else if (!wide_) {                   \
+                call(FCfg<5>);                     \
+            } else if (bits_ == 2) {               \
+                call(M3_F32(2));                   \
+            } else if (bits_ == 3) {               \
+                call(M3_F32(3));                   \
+            } else if (bits_ == 4) {               \
+                call(M3_F32(4));                   \
+            } else {                               \
+                call(M3_F32(5));                   \
             }                                      \
         }                                          \
     } while (0)
 
 extern "C" {
 int hc_set_frame(int rows, int columns, int types) {
-    if (rows < 3 || rows > 16 || columns < 3 || columns > 16 || types < 2 || types > 15) return -1;
+    if (rows < 3 || rows > MAX_FRAME || columns < 3 || columns > MAX_FRAME || types < 2 || types > 31) return -1;
     g_T = types;
     g_shape = make_shape(rows, columns, types);
     return 0;

@@ -44,7 +44,12 @@ def test_loads_and_reports_shapes():
     assert _native.supported(7, 7, 5) and _native.supported(3, 3, 3) and _native.supported(16, 3, 15)
     assert _native.supported(9, 9, 2) and _native.supported(5, 5, 2)
     assert _native.supported(8, 10, 5)  # rows < columns: resets only (the reference raises on a step)
-    for bad in ((2, 9, 6), (9, 17, 6), (17, 9, 6), (9, 9, 16), (9, 9, 1)):
+    # a side above 16: the 32 x 32 frame
+    assert _native.supported(20, 20, 6) and _native.supported(17, 9, 6) and _native.supported(32, 32, 15)
+    assert _native.supported(9, 17, 6) and _native.supported(32, 3, 4)
+    # types 16..31: the 5-bit token layout
+    assert _native.supported(9, 9, 16) and _native.supported(12, 12, 31) and _native.supported(20, 20, 24)
+    for bad in ((2, 9, 6), (33, 9, 6), (9, 33, 6), (9, 9, 32), (9, 9, 1)):
         assert not _native.supported(*bad), bad
     a, w = np.zeros(1, np.int32), np.zeros(1, np.int32)
     _native.check(L.m3_action_space(9, 9, _native.ptr(a), _native.ptr(w)))
@@ -61,5 +66,5 @@ def test_fails_loudly_without_gpu():
 
 def test_unsupported_shape_error():
     with pytest.raises(_native.M3Error) as e:
-        _native.Context(17, 9, 6)
+        _native.Context(33, 9, 6)
     assert e.value.code == -2

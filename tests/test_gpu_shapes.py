@@ -42,26 +42,26 @@ def test_fixture_covers_the_asked_shapes(golden):
     assert set(_tags(g, "wide_seeds_")) == {"8x10x5", "3x5x3"}
 
 
-def test_frame_shapes_golden(golden):
-    g = golden("shapes")
-    for tag in _tags(g, "init_seeds_"):
-        R, C, T = _shape(tag)
-        ctx = _native.Context(R, C, T)
-        A = ctx.A
-        boards, draws, _ = ctx.init_boards(g["init_seeds_" + tag].astype(np.uint32))
-        assert (boards == g["init_boards_" + tag]).all(), tag
-        assert (draws == g["init_draws_" + tag]).all(), tag
-        bits = unpack(ctx.legal_bits(g["legal_boards_" + tag]), A)
-        assert (bits == g["legal_" + tag]).all(), tag
-        ok = g["step_draws_" + tag] != -2  # (-2: the reference hangs in a cycling shuffle)
-        r = ctx.apply_actions(g["step_board_" + tag][ok], g["step_seed_" + tag][ok], g["step_n_actions_" + tag][ok],
-                              g["step_action_" + tag][ok])
-        assert (r["boards"] == g["step_next_" + tag][ok]).all(), tag
-        assert (r["reward"] == g["step_reward_" + tag][ok]).all(), tag
-        live = g["step_draws_" + tag][ok] >= 0
-        assert (r["draws"][live] == g["step_draws_" + tag][ok][live]).all(), tag
-        # seeded random_task episodes through the batched env (its step / reset / random-action kernels)
-        seeds = g["ep_seeds_" + tag].astype(np.uint32)
+def _check_golden_shape(g, tag):
+    """init / legal / apply_action / seeded-episode fixtures of one BoardConfig through the C-ABI"""
+    R, C, T = _shape(tag)
+    ctx = _native.Context(R, C, T)
+    A = ctx.A
+    boards, draws, _ = ctx.init_boards(g["init_seeds_" + tag].astype(np.uint32))
+    assert (boards == g["init_boards_" + tag]).all(), tag
+    assert (draws == g["init_draws_" + tag]).all(), tag
+    bits = unpack(ctx.legal_bits(g["legal_boards_" + tag]), A)
+    assert (bits == g["legal_" + tag]).all(), tag
+    ok = g["step_draws_" + tag] != -2  # (-2: the reference hangs in a cycling shuffle)
+    r = ctx.apply_actions(g["step_board_" + tag][ok], g["step_seed_" + tag][ok], g["step_n_actions_" + tag][ok],
+                          g["step_action_" + tag][ok])
+    assert (r["boards"] == g["step_next_" + tag][ok]).all(), tag
+    assert (r["reward"] == g["step_reward_" + tag][ok]).all(), tag
+    live = g["step_draws_" + tag][ok] >= 0
+    assert (r["draws"][live] == g["step_draws_" + tag][ok][live]).all(), tag
+    # seeded random_task episodes through the batched env (its step / reset / random-action kernels)
+    seeds = g["ep_seeds_" + tag].astype(np.uint32)
+    if len(seeds):
         env = BatchedMatch3Env(len(seeds), R, C, T, num_moves=20, env_goal=BIG, seeds=seeds, autoreset=False)
         assert (env.observations() == g["ep_init_" + tag]).all(), tag
         for m in range(20):
@@ -71,7 +71,40 @@ def test_frame_shapes_golden(golden):
             assert (env.draws() == g["ep_draws_" + tag][:, m]).all(), (tag, m)
         assert (env.observations() == g["ep_final_" + tag]).all(), tag
         env.close()
-        ctx.close()
+    ctx.close()
+
+
+def test_frame_shapes_golden(golden):
+    g = golden("shapes")
+    for tag in _tags(g, "init_seeds_"):
+        _check_golden_shape(g, tag)
+
+
+def test_big_boards_golden(golden):
+    """Boards past 16 x 16 (the 32 x 32 frame, FCfg<BITS, 32>): 20x20x6, 24x17x5, 17x17x3 and
+    32x32x8, and types 16..31 (5 token bits, FCfg<5>): 9x9x20, 12x12x31, against
+    tests/golden/big.npz (gen_golden.py: gen_big). 17x17x3 has no episodes: the
+    reference's seeded play there runs into cascades it does not finish within the generator's
+    5 s per episode."""
+    g = golden("big")
+    tags = _tags(g, "init_seeds_")
+    assert {"20x20x6", "24x17x5", "32x32x8", "17x17x3", "9x9x20", "12x12x31"} <= set(tags)
+    for tag in tags:
+        _check_golden_shape(g, tag)
+
+
+def test_big_boards_rollouts_vs_oracle():
+    """MCTS rollouts on 20x20x6 (one 32 x 32-frame board per lane, whole waves) against the oracle."""
+    R, C, T = 20, 20, 6
+    ctx = _native.Context(R, C, T)
+    seeds = np.arange(1, 257, dtype=np.uint32)
+    boards, _, _ = ctx.init_boards(seeds)
+    rs = (np.arange(256, dtype=np.uint64) * 2654435761 % (2**31)).astype(np.uint32)
+    ro = ctx.rollouts(boards, seeds, 20, rs)
+    want = Oracle(R, C, T).rollouts(boards.astype(np.int32), seeds, 20, rs, threads=4)
+    assert (ro["gain"] == want["gain"]).all() and (ro["steps"] == want["steps"]).all()
+    assert (ro["draws"] == want["draws"]).all()
+    ctx.close()
 
 
 def test_rows_below_columns_reset_but_do_not_step(golden):
@@ -133,9 +166,14 @@ def test_frame_env_large_batch_vs_oracle(shape):
     env.close()
 
 
-def test_frame_rollouts_and_autoreset_vs_oracle():
-    """MCTS rollouts (f3) and same-step autoreset (f1) on a frame shape."""
-    R, C, T = 10, 8, 5
+@pytest.mark.parametrize("shape", [(10, 8, 5), (12, 12, 7), (10, 10, 6), (10, 8, 9), (16, 16, 15)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_frame_rollouts_vs_oracle(shape):
+    """MCTS rollouts (f3) of 4096 states, 64 lanes a wave, on frame shapes of every token width.
+    (Regression: with ~1,500 SGPR spills in k_rollout some of these shapes came out wrong for a
+    lane only when other lanes of its wave were active -- the frame action-id packing now runs as
+    a rolled loop, tools/dbg.)"""
+    R, C, T = shape
     ctx = _native.Context(R, C, T)
     seeds = np.arange(1, 4097, dtype=np.uint32)
     boards, _, _ = ctx.init_boards(seeds)
@@ -144,6 +182,13 @@ def test_frame_rollouts_and_autoreset_vs_oracle():
     want = Oracle(R, C, T).rollouts(boards.astype(np.int32), seeds, 20, rs, threads=4)
     assert (ro["gain"] == want["gain"]).all() and (ro["steps"] == want["steps"]).all()
     assert (ro["draws"] == want["draws"]).all()
+    ctx.close()
+
+
+def test_frame_autoreset_vs_oracle():
+    """Same-step autoreset (f1) on a frame shape."""
+    R, C, T = 10, 8, 5
+    ctx = _native.Context(R, C, T)
     n = 2048
     env = BatchedMatch3Env(n, R, C, T, num_moves=5, env_goal=BIG, seed_base=100, autoreset=True, seed_stride=n)
     for _ in range(5):

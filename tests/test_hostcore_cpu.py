@@ -302,3 +302,34 @@ def test_frame_rows_below_columns_reset_only(golden):
         R, C, T = (int(x) for x in tag.split("x"))
         out, drw, _, _ = HostCore(R, C, T).init(g["wide_seeds_" + tag].astype(np.uint32))
         assert (out == g["wide_boards_" + tag].reshape(len(out), -1)).all() and (drw == g["wide_draws_" + tag]).all()
+
+
+def test_wide_frame_big_boards_golden(golden):
+    """The 32 x 32 frame (boards with a side > 16) on the host against tests/golden/big.npz:
+    resets, legal sets, apply_action transitions and seeded episodes of 20x20x6, 24x17x5, 17x17x3
+    and 32x32x8, and the 5-bit token layouts of 9x9x20 and 12x12x31 (types 16..31)."""
+    g = golden("big")
+    for tag in ("20x20x6", "24x17x5", "17x17x3", "32x32x8", "9x9x20", "12x12x31"):
+        R, C, T = (int(x) for x in tag.split("x"))
+        hc = HostCore(R, C, T)
+        assert hc.frame
+        out, drw, _, _ = hc.init(g["init_seeds_" + tag].astype(np.uint32))
+        assert (out == g["init_boards_" + tag].reshape(len(out), -1)).all() and (drw == g["init_draws_" + tag]).all()
+        bits = np.unpackbits(hc.legal(g["legal_boards_" + tag]).view(np.uint8), axis=1, bitorder="little")
+        assert (bits[:, :hc.A] == g["legal_" + tag]).all(), tag
+        ok = g["step_draws_" + tag] != -2
+        out, rew, drw, _, _, _ = hc.apply(g["step_board_" + tag][ok], g["step_seed_" + tag][ok],
+                                          g["step_n_actions_" + tag][ok], g["step_action_" + tag][ok], small=32)
+        assert (out == g["step_next_" + tag][ok].reshape(len(out), -1)).all(), tag
+        assert (rew == g["step_reward_" + tag][ok]).all(), tag
+        live = g["step_draws_" + tag][ok] >= 0
+        assert (drw[live] == g["step_draws_" + tag][ok][live]).all(), tag
+        seeds = g["ep_seeds_" + tag].astype(np.uint32)
+        if not len(seeds):
+            continue
+        b, _, _, act = hc.init(seeds)
+        for mv in range(20):
+            assert (act == g["ep_actions_" + tag][:, mv]).all(), (tag, mv)
+            b, rew, drw, _, _, act = hc.apply(b, seeds, 20 - mv, act, small=32)
+            assert (rew == g["ep_rewards_" + tag][:, mv]).all() and (drw == g["ep_draws_" + tag][:, mv]).all()
+        assert (b == g["ep_final_" + tag].reshape(len(b), -1)).all(), tag

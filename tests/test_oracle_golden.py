@@ -88,11 +88,11 @@ def test_shuffle_path(golden, tag):
     assert n_shuffled > 100
 
 
-@pytest.mark.parametrize("fixture", ["shapes", "types2"])
+@pytest.mark.parametrize("fixture", ["shapes", "types2", "big"])
 def test_other_board_configs(golden, fixture):
     """Every other BoardConfig the fixtures hold (shapes.npz: square, rows > columns, 3 and 15
-    types; types2.npz: two tile types), through the oracle: resets, legal sets, transitions and
-    seeded episodes."""
+    types; types2.npz: two tile types; big.npz: sides 17..32 and types 20 / 31), through the
+    oracle: resets, legal sets, transitions and seeded episodes."""
     g = golden(fixture)
     tags = sorted({k[len("init_seeds_"):] for k in g.files if k.startswith("init_seeds_")})
     assert tags

@@ -9,7 +9,7 @@ TAG=${1:-dev}; shift
 O=gpurun_out/$TAG; mkdir -p $O
 S16="--shape 16x16x8 --boards 262144"
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+  timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $O/gpu_tests.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -3 $O/gpu_tests.log
   [ $rc -eq 0 ] || exit 1
 fi
