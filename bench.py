@@ -438,7 +438,7 @@ def main():
         # one shard's step pipeline: k_env_step + k_env_cont (the continuation of the
         # long cascades) + k_env_fix (dead boards, recomputes), bracketed by HIP events
         # on the shard's stream
-        "kernel": "k_env_step + k_env_cont + k_env_fix",
+        "kernel": "k_env_step + k_env_cont_grid + k_env_fix",
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic, "algorithmic_bytes_per_launch": bytes_per_launch, "boards_per_launch": shard_boards,
         "avg_kernel_ms": avg_kernel_s * 1e3,

@@ -7,7 +7,7 @@ Writes profiles/<round-tag>_bench.json (the bench line), <round-tag>_kernel_stat
 (rocprofv3 --kernel-trace --stats of the same bench command), <round-tag>_pmc.txt
 (per-kernel PMC means, one rocprofv3 pass per counter group) and traffic.json
 (traffic_<shape>.json for a shape other than 9x9x6):
-HBM bytes per launch of one shard's step pipeline (k_env_step + k_env_cont + k_env_fix, the
+HBM bytes per launch of one shard's step pipeline (k_env_step + k_env_cont(_grid) + k_env_fix, the
 two kernels bench.py's HIP events bracket) = 2 * FETCH_SIZE + WRITE_SIZE (KB ->
 bytes), the factor 2 being MI355X_MICROARCH.md's gfx950 correction for wide
 coalesced reads (FETCH_SIZE reports half of them; narrower accesses are
@@ -39,9 +39,9 @@ pmc = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.p
                      capture_output=True, text=True, check=True).stdout
 open(os.path.join(P, f"{tag}_pmc.txt"), "w").write(pmc)
 
-PIPE = ("k_env_step", "k_env_cont", "k_env_fix")
+PIPE = ("k_env_step", "k_env_cont", "k_env_cont_grid", "k_env_fix")
 # every kernel that runs inside a timed step: the step pipeline and the autoreset (prefetch) kernels
-STEP_KERNELS = PIPE + ("k_env_cont_grid", "k_init", "k_init_coop", "k_init_fix_lane", "k_init_chain2")
+STEP_KERNELS = PIPE + ("k_init", "k_init_coop", "k_init_fix_lane", "k_init_chain2")
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 allk = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{src}/**/*_counter_collection.csv", recursive=True):
@@ -77,7 +77,8 @@ fetch = per_launch("FETCH_SIZE") * 1024
 write = per_launch("WRITE_SIZE") * 1024
 cfg = bench["config"]
 rl = bench["roofline"].get("hbm", bench["roofline"])  # (the HBM block sits inside a VALU-bound roofline)
-traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"], "kernel": "k_env_step + k_env_cont + k_env_fix",
+traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"],
+           "kernel": "k_env_step + k_env_cont(_grid) + k_env_fix (the kernels of one shard's step pipeline)",
            "boards_per_launch": rl.get("boards_per_launch"),
            "fetch_size_bytes": fetch, "write_size_bytes": write,
            "hbm_bytes_per_launch": 2 * fetch + write,
