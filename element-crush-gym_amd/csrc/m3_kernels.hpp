@@ -118,8 +118,8 @@ struct KS {
     static constexpr int CONT_WPS = CF::N > 128 ? 1 : M3_CONT_WPS;
     // 1: k_env_step waves that finish their own boards take paused steps from the shard's queue
     // (work-stealing tail, k_env_step phase 2); k_env_cont then only finishes the dead boards.
-    // Off: exact, but 9x9x6 ran at 67 ms/step against 0.46 with the separate k_env_cont launch
-    // (gpurun_out/r04g)
+    // 2: the same with a write-through hand-off (no fence). Off: both exact, both ~67 ms/step at
+    // 9x9x6 against 0.46 with the separate k_env_cont launch (gpurun_out/r04g, r04j)
 #ifndef M3_FUSED_CONT
 #define M3_FUSED_CONT 0
 #endif
@@ -359,6 +359,22 @@ __device__ __forceinline__ bool block_copy_in_checked(const int8_t* __restrict__
 // zero-copy path of small host-buffer calls, where device atomics are not an option)
 __device__ __forceinline__ void flag_bad_cells(bool bad, uint32_t* flag) {
     if (flag && __any((int)bad) && __lane_id() == 0) *(volatile uint32_t*)flag = 1u;
+}
+
+// device-coherent word store / load (relaxed, agent scope: written through / read past the XCD's L2,
+// no cache-wide write-back or invalidate) -- the M3_FUSED_CONT=2 hand-off
+__device__ __forceinline__ void st_dev(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ uint32_t ld_dev(uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// block_copy_out through device-coherent stores (the block start is 4-byte aligned; tail bytes one by one)
+template <int BLOCK>
+__device__ __forceinline__ void block_copy_out_dev(int8_t* __restrict__ g, const uint8_t* lds, int bytes) {
+    const int n4 = bytes >> 2;
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(lds);
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(g);
+    for (int i = threadIdx.x; i < n4; i += BLOCK) st_dev(d4 + i, s4[i]);
+    for (int i = (n4 << 2) + threadIdx.x; i < bytes; i += BLOCK)
+        __hip_atomic_store(reinterpret_cast<uint8_t*>(g) + i, lds[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int BLOCK>
@@ -1317,7 +1333,11 @@ constexpr uint32_t CONT_EMPTY = 0xFFFFFFFFu;
 template <class CF, class RNG>
 __device__ __forceinline__ void cont_write(uint32_t* rec, int64_t cs, const typename CF::Bd* P, const RNG& rng, int r,
                                            uint32_t f) {
-    Cont<CF, RNG>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
+    if constexpr (M3_FUSED_CONT == 2) {
+        Cont<CF, RNG>::save(P, rng, r, f, [&](int i, uint32_t w) { st_dev(rec + (int64_t)(i + 1) * cs, w); });
+    } else {
+        Cont<CF, RNG>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
+    }
 }
 
 // a settled board with no legal move: the dead queue, from the top of the record area down
@@ -1360,15 +1380,21 @@ __device__ __forceinline__ void env_steal(const EnvArgs& a, Store& st, const typ
         if ((uint32_t)t < k) {
             uint32_t* rec = a.cont + base + t;
             uint32_t bw;
-            while ((bw = __hip_atomic_load(rec, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == CONT_EMPTY)
-                __builtin_amdgcn_s_sleep(2);
+            if constexpr (M3_FUSED_CONT == 2) {
+                while ((bw = ld_dev(rec)) == CONT_EMPTY) __builtin_amdgcn_s_sleep(2);
+            } else {
+                while ((bw = __hip_atomic_load(rec, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == CONT_EMPTY)
+                    __builtin_amdgcn_s_sleep(2);
+            }
             const int64_t b = bw;
             const int64_t cs = a.cont_stride;
             typename CF::Bd P[CF::NP], HL, VL;
             typename K::Rng rng;
             int r;
             uint32_t f;
-            EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
+            EnvCont<CF>::load(P, rng, r, f, [&](int i) {
+                return M3_FUSED_CONT == 2 ? ld_dev(rec + (int64_t)(i + 1) * cs) : rec[(int64_t)(i + 1) * cs];
+            });
             rec[0] = CONT_EMPTY;
             const int mv = a.moves[b], sc0 = a.score[b];
             const int c = apply_cascade_ex<CF, CASX_STOP_DEAD>(P, rng, f, HL, VL, st, r, -1, false, dm);
@@ -1493,12 +1519,23 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
         }
     }
     lds_sync();
-    block_copy_out<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
-    if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT) {
+    if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT == 2) {
+        // boards and records written through (device-coherent stores), waited for, then the record
+        // is marked ready: no cache-wide maintenance, and a stolen board's final bytes (the stealer's
+        // ordinary stores) land after the owner's copy
+        block_copy_out_dev<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
+        __builtin_amdgcn_s_waitcnt(0);
+        if (pub_q != ~0u) st_dev(a.cont + pub_q, pub_b);
+    } else {
+        block_copy_out<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
+    }
+    if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT == 1) {
         if (pub_q != ~0u) {  // the board stores above are visible before the record is marked ready
             __threadfence();
             __hip_atomic_store(a.cont + pub_q, pub_b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+    if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT) {
         lds_sync();  // the group table reuses the staging area
         env_steal<CF>(a, st, dm);
     }
