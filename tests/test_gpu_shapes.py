@@ -251,3 +251,37 @@ def test_two_types_large_board_steps_return_flagged(golden):
     assert np.isin(obs[~capped], [1, 2, 4, 8, 12, 16]).all()  # tiles 1..2, H 4, V 8, B 12, M 16 (TM 3)
     assert np.isin(obs[capped], [0, 1, 2, 4, 8, 12, 16]).all()  # (a capped cascade stops with its holes)
     env.close()
+
+
+@pytest.mark.parametrize("shape", [(6, 6, 5), (9, 9, 7), (11, 11, 8), (13, 13, 9), (16, 16, 12), (16, 9, 7),
+                                   (10, 3, 4), (12, 12, 20)], ids=lambda s: "x".join(map(str, s)))
+def test_frame_full_waves_episodes_and_rollouts_vs_oracle(shape):
+    """Every lane of every wave busy (4,096 boards): 20 seeded random-action env moves and then a
+    20-move rollout from each final board, against the oracle -- the lane-interference guard of
+    DESIGN.md §4 ("SGPR spills") on frame shapes of every token width (tools/dbg/frame_sweep.py
+    runs 24 shapes)."""
+    R, C, T = shape
+    n = 4096
+    seeds = np.arange(1, n + 1, dtype=np.uint32)
+    env = BatchedMatch3Env(n, R, C, T, num_moves=20, env_goal=BIG, seeds=seeds, autoreset=False)
+    acts, rews = [], []
+    for _ in range(20):
+        acts.append(env.next_actions())
+        env.step()
+        rews.append(env.rewards())
+    o = Oracle(R, C, T, episode_shuffle_cap=1024).batch_episodes(seeds, 20, BIG)
+    cap = (env.flags() & (_native.FLAG_SHUFFLE_CAP | _native.FLAG_CASCADE_CAP)) != 0
+    ok = (o["moves"] == 20) & ~cap
+    assert ok.mean() > 0.85
+    assert (np.array(acts).T[ok] == o["actions"][ok]).all()
+    assert (np.array(rews).T[ok] == o["rewards"][ok]).all()
+    fin = env.observations().reshape(n, R, C).astype(np.int8)
+    assert (fin.reshape(n, -1)[ok] == o["final"][ok]).all()
+    env.close()
+    ctx = _native.Context(R, C, T)
+    rs = (np.arange(n, dtype=np.uint64) * 2654435761 % (2**31)).astype(np.uint32)
+    ro = ctx.rollouts(fin, seeds, 20, rs)
+    want = Oracle(R, C, T).rollouts(fin.astype(np.int32), seeds, 20, rs)
+    assert (ro["gain"] == want["gain"]).all() and (ro["steps"] == want["steps"]).all()
+    assert (ro["draws"] == want["draws"]).all()
+    ctx.close()
