@@ -76,15 +76,26 @@ def cpu_baseline(rows, cols, types, moves, goal, seconds):
            "sample": f"{n} seeded {rows}x{cols}x{types} random-action episodes of {moves} moves "
                      f"(init + legal_actions + choice + apply_action per move; {steps} steps, {dt:.1f} s), "
                      f"oracle/m3_oracle.c, OpenMP over episodes on {threads} threads"}
+    # the same port on ONE core (the C restatement timed on all host cores and on 1 core),
+    # a quarter of the sample time
+    n1 = max(256, int(probe * seconds / 4 / max(dt / n * probe * threads, 1e-3)))
+    seeds1 = list(range(3 * 10**6, 3 * 10**6 + n1))
+    t0 = time.perf_counter()
+    steps1, _ = o.run_episodes(seeds1, moves, goal, 1)
+    dt1 = time.perf_counter() - t0
+    res["one_core"] = {"value": steps1 / dt1, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                       "sample": f"{n1} episodes ({steps1} steps, {dt1:.1f} s), oracle/m3_oracle.c on 1 thread"}
     try:  # C port here / reference Python here, both measured in the build container (tools/calibrate_cpu.py)
         with open(os.path.join(ROOT, "profiles", "cpu_calibration.json")) as f:
             cal = json.load(f)
         if (rows, cols, types) == (9, 9, 6):
-            res["reference_python_equiv"] = {
-                "value": res["value"] * cal["ratio_1core"], "unit": "env-steps/s",
-                "how": "this host's C-port rate x (reference Python / C port per core, both timed on "
-                       f"{cal['cores']} build-container cores: {cal['ref_python_1']['env_steps_per_s']:.0f} / "
-                       f"{cal['c_port_1']['env_steps_per_s']:.0f} env-steps/s), profiles/cpu_calibration.json"}
+            how = ("this host's C-port rate x (reference Python / C port per core, both timed on "
+                   f"{cal['cores']} build-container cores: {cal['ref_python_1']['env_steps_per_s']:.0f} / "
+                   f"{cal['c_port_1']['env_steps_per_s']:.0f} env-steps/s), profiles/cpu_calibration.json")
+            res["reference_python_equiv"] = {"value": res["value"] * cal["ratio_1core"], "unit": "env-steps/s",
+                                             "cores": threads, "how": how}
+            res["one_core"]["reference_python_equiv"] = {"value": res["one_core"]["value"] * cal["ratio_1core"],
+                                                         "unit": "env-steps/s", "cores": 1, "how": how}
     except (OSError, KeyError, ValueError):
         pass
     return res
@@ -156,6 +167,33 @@ def gather_check(env, dist, rank, world):
     return all(dist.allgather_obj(ok))
 
 
+def step_fns(env, world, mode):
+    """(step, on_end) of the timed region: one env step per call; for N > 1 the RCCL all-gather of the
+    packed outcome words after every step (mode "step") or once after the last timed step ("final")."""
+    def step():
+        env.step()
+        if world > 1 and mode == "step":
+            env.gather()
+
+    return step, ((lambda: env.gather()) if world > 1 and mode == "final" else None)
+
+
+class _StubEnv:
+    """--dry-rendezvous: counts what the timed region would enqueue (no device)."""
+
+    def __init__(self):
+        self.steps = self.gathers = 0
+
+    def step(self):
+        self.steps += 1
+
+    def gather(self):
+        self.gathers += 1
+
+    def synchronize(self):
+        pass
+
+
 def spawn_ranks(args):
     """`bench.py --gpus N` without a launcher: start N rank processes (RANK = LOCAL_RANK = device),
     host their rendezvous here, and exit with the first failing rank's code (the other ranks are
@@ -219,6 +257,7 @@ def oracle_sample_check(env, shape, moves, goal, seed_base, stride, total_steps,
         idx = np.unique(np.linspace(0, n - 1, k).astype(np.int64))
     obs = env.observations().reshape(n, -1)
     score, mv, seeds, nxt = env.scores(), env.moves(), env.seeds(), env.next_actions()
+    dev_flags = env.flags()
     bad = capped = 0
     for b in idx:
         rem, e = total_steps, 0
@@ -226,17 +265,19 @@ def oracle_sample_check(env, shape, moves, goal, seed_base, stride, total_steps,
         while True:
             seed = (seed_base + int(b) + e * stride) & 0xFFFFFFFF
             ep = o.random_episode(seed, moves, goal)
-            if ep["flags"] & SHUFFLE_CAP_FLAG:
-                break
-            if ep["n"] <= rem:
+            if ep["n"] <= rem:  # a whole episode inside the replayed steps: its cap matters
+                if ep["flags"] & SHUFFLE_CAP_FLAG:
+                    break
                 rem -= ep["n"]
                 e += 1
                 if rem == 0:  # autoreset in the step that finished the episode
                     seed = (seed + stride) & 0xFFFFFFFF
                     want = (o.init_board(seed)[0].reshape(-1), 0, 0, seed, o.random_episode(seed, 1, goal)["actions"][0])
                     break
-            else:
+            else:  # the replay ends inside this episode: only its first `rem` steps (and the next action) count
                 part = o.random_episode(seed, rem, goal)
+                if part["flags"] & SHUFFLE_CAP_FLAG:
+                    break
                 want = (part["final"].reshape(-1), int(part["rewards"].sum()), rem, seed, ep["actions"][rem])
                 break
         if want is None:
@@ -244,8 +285,11 @@ def oracle_sample_check(env, shape, moves, goal, seed_base, stride, total_steps,
             continue
         got = (obs[b], score[b], mv[b], seeds[b], nxt[b])
         bad += not ((got[0] == want[0]).all() and all(int(x) == int(y) for x, y in zip(got[1:], want[1:])))
+    # boards the device itself flagged at the shuffle cap in the last step (their replay is in `shuffle_capped`
+    # when the oracle hits the cap within the replayed steps too)
+    dev_capped = int(((dev_flags[idx] & SHUFFLE_CAP_FLAG) != 0).sum())
     return {"boards": int(len(idx)) - capped, "mismatches": int(bad), "steps_replayed": total_steps,
-            "shuffle_capped": capped}
+            "shuffle_capped": capped, "device_shuffle_capped_last_step": dev_capped}
 
 
 def bench_rollouts(a):
@@ -333,6 +377,10 @@ def main():
                          "what each rank received and exit before any GPU work (tests/test_bench_cpu.py)")
     ap.add_argument("--check-boards", type=int, default=256,
                     help="boards per rank replayed through the C oracle after the clock stops (0: none)")
+    ap.add_argument("--gather", choices=("final", "step"), default="final",
+                    help="N > 1: RCCL all-gather of the packed reward/truncated/done words once, after the last "
+                         "timed step (final: BASELINE north_star's 'final reward/done gather', the headline) or "
+                         "after every step (step); both inside the timed region")
     ap.add_argument("--allow-stale-lib", action="store_true",
                     help="if `make` fails, time the library already built (recorded as build.stale in the line)")
     args = ap.parse_args()
@@ -361,7 +409,13 @@ def main():
         import hashlib
 
         uid = share_unique_id(dist, rank, lambda: os.urandom(128)) if dist else os.urandom(128)
-        line = json.dumps({"rank": rank, "world": world, "local_rank": local,
+        from match3tile.distributed import timed_steps
+
+        stub = _StubEnv()
+        st, end = step_fns(stub, world, args.gather)
+        timed_steps(st, stub.synchronize, args.steps, args.warmup, dist, on_end=end)
+        line = json.dumps({"rank": rank, "world": world, "local_rank": local, "gather": args.gather,
+                           "stub_steps": stub.steps, "stub_gathers": stub.gathers,
                            "dist_world": dist.get_world_size() if dist else 1,
                            "spawned": os.environ.get("M3_SPAWNED") == "1", "torch_loaded": "torch" in sys.modules,
                            "id_bytes": len(uid), "id_sha256": hashlib.sha256(uid).hexdigest()})
@@ -407,13 +461,11 @@ def main():
     if dist:
         env.init_comm(uid, world, rank)
 
-    def step():
-        env.step()
-        if world > 1:
-            env.gather()
-
-    elapsed = timed_steps(step, env.synchronize, args.steps, args.warmup, dist,
-                          on_start=lambda: env.enable_timing(args.steps))
+    step, final_gather = step_fns(env, world, args.gather)
+    elapsed, elapsed_local = timed_steps(step, env.synchronize, args.steps, args.warmup, dist,
+                                         on_start=lambda: env.enable_timing(args.steps), on_end=final_gather,
+                                         return_local=True)
+    rank_ms = dist.allgather_obj(elapsed_local / args.steps * 1e3) if dist else [elapsed_local / args.steps * 1e3]
     kms = env.kernel_ms()
     stats = env.stats()
     # ---- after the clock: attest the run (nothing below is timed) ----
@@ -491,7 +543,8 @@ def main():
                 "(samplerTasks.random_task contract), 20-move episodes, autoreset with seed += n_boards",
         "config": {
             "workload": f"{'C3' if (rows, cols) == (9, 9) else 'C4'}: {B:,} boards per GPU, {rows}x{cols}x{types}, Match3Env.step x {args.steps} "
-                        "(step kernel + overflow fixup + autoreset; RCCL reward/done all-gather when N>1)",
+                        "(step kernel + overflow fixup + autoreset; N>1: RCCL reward/done all-gather "
+                        + ("once after the last step" if args.gather == "final" else "after every step") + ")",
             "boards_per_gpu": B,
             "shape": args.shape,
             "num_moves": args.moves,
@@ -502,6 +555,8 @@ def main():
             "autoreset": not args.no_autoreset,
         },
         "nranks": nranks,
+        "gather": (args.gather if world > 1 else None),
+        "ms_per_step_per_rank": rank_ms,
         "gather_ok": gather_ok,
         "parity": parity,
         "path_stats": {"autoresets": stats["autoresets"], "reset_recomputes": stats["reset_recomputes"],

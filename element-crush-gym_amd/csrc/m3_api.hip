@@ -21,14 +21,18 @@ int set_err(int code, const char* fmt, ...) {
 namespace m3k {
 M3_INSTANTIATE(extern template, CF_0)
 M3_INSTANTIATE(extern template, CF_1)
+#ifndef M3_HEADLINE_ONLY  // A/B builds of the two specialised shapes only (Makefile `variant-fast`)
 M3_INSTANTIATE(extern template, CF_2)
 M3_INSTANTIATE(extern template, CF_3)
 M3_INSTANTIATE(extern template, CF_4)
 M3_INSTANTIATE(extern template, CF_5)
+#ifndef M3_NO_WIDE_FRAME  // (Makefile `variant-frame16`: no 32 x 32 frame)
 M3_INSTANTIATE(extern template, CF_6)
 M3_INSTANTIATE(extern template, CF_7)
 M3_INSTANTIATE(extern template, CF_8)
 M3_INSTANTIATE(extern template, CF_9)
+#endif
+#endif
 }  // namespace m3k
 #endif
 using namespace m3k;
@@ -207,14 +211,18 @@ static int with_shape(int shape, F&& f) {
     switch (shape) {
         case 0: return f(CF_0{});
         case 1: return f(CF_1{});
+#ifndef M3_HEADLINE_ONLY
         case 2: return f(CF_2{});
         case 3: return f(CF_3{});
         case 4: return f(CF_4{});
         case 5: return f(CF_5{});
+#ifndef M3_NO_WIDE_FRAME
         case 6: return f(CF_6{});
         case 7: return f(CF_7{});
         case 8: return f(CF_8{});
         case 9: return f(CF_9{});
+#endif
+#endif
         default: return set_err(M3_ERR_UNSUPPORTED, "board shape not compiled in");
     }
 }
@@ -331,15 +339,15 @@ int m3_dev_copy(m3_ctx* c, void* dst, const void* src, int64_t bytes, int kind) 
     return M3_OK;
 }
 
-int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boards, uint32_t* out_draws,
-                   int32_t* out_first_action) {
+int m3_init_boards_ex(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boards, uint32_t* out_draws,
+                      int32_t* out_first_action, uint32_t* out_flags) {
     CHECK_ARG(c && n >= 0 && (n == 0 || (seeds && out_boards)), "bad arguments");
     if (n == 0) return M3_OK;
     HIP_TRY(hipSetDevice(c->device));
     if (n <= ZC_MAX_BOARDS) {  // zero-copy: the reset launch(es) and one sync
         Image im;
         const int i_s = im.add(n * 4ull), o_b = im.add(n * (size_t)c->N), o_d = im.add(n * 4ull),
-                  o_f = im.add(n * 4ull);
+                  o_f = im.add(n * 4ull), o_g = im.add(n * 4ull);
         int rc = ensure_host(c, im.total + 256);
         if (rc) return rc;
         char* h = (char*)c->hbuf;
@@ -352,17 +360,20 @@ int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boar
         a.boards = (int8_t*)(d + im.off[o_b]);
         a.draws = (uint32_t*)(d + im.off[o_d]);
         a.first_action = (int32_t*)(d + im.off[o_f]);
+        a.flags = (uint32_t*)(d + im.off[o_g]);
         rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, n); });
         if (rc) return rc;
         HIP_TRY(hipStreamSynchronize(c->stream));
         memcpy(out_boards, h + im.off[o_b], n * (size_t)c->N);
         if (out_draws) memcpy(out_draws, h + im.off[o_d], n * 4);
         if (out_first_action) memcpy(out_first_action, h + im.off[o_f], n * 4);
+        if (out_flags) memcpy(out_flags, h + im.off[o_g], n * 4);
         return M3_OK;
     }
     Image in, out;
     in.add(n * 4ull);
-    const int o_b = out.add(n * (size_t)c->N), o_d = out.add(n * 4ull), o_f = out.add(n * 4ull);
+    const int o_b = out.add(n * (size_t)c->N), o_d = out.add(n * 4ull), o_f = out.add(n * 4ull),
+              o_g = out.add(n * 4ull);
     char* dev;
     int rc = stage_begin(c, in, out, 0, &dev);
     if (rc) return rc;
@@ -376,9 +387,23 @@ int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boar
     a.boards = (int8_t*)(dout + out.off[o_b]);
     a.draws = (uint32_t*)(dout + out.off[o_d]);
     a.first_action = (int32_t*)(dout + out.off[o_f]);
+    a.flags = (uint32_t*)(dout + out.off[o_g]);
     rc = with_shape(c->shape, [&](auto cf) { return launch_init<decltype(cf)>(c->stream, a, n); });
     if (rc) return rc;
-    return stage_download(c, out, {out_boards, out_draws, out_first_action}, dout);
+    return stage_download(c, out, {out_boards, out_draws, out_first_action, out_flags}, dout);
+}
+
+int m3_init_boards(m3_ctx* c, int64_t n, const uint32_t* seeds, int8_t* out_boards, uint32_t* out_draws,
+                   int32_t* out_first_action) {
+    std::vector<uint32_t> flags(n > 0 ? (size_t)n : 0);
+    int rc = m3_init_boards_ex(c, n, seeds, out_boards, out_draws, out_first_action, flags.data());
+    if (rc) return rc;
+    int64_t capped = 0;
+    for (uint32_t f : flags) capped += (f & M3_FLAG_RESET_CAP) != 0;
+    if (capped)  // the reference keeps drawing (boardv2.py:23-27): no result to return
+        return set_err(M3_ERR_CAP, "%lld of %lld resets stopped at the redraw-round cap (M3_FLAG_RESET_CAP; "
+                       "m3_init_boards_ex returns the flags per board)", (long long)capped, (long long)n);
+    return M3_OK;
 }
 
 int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t* seeds, const int32_t* n_actions,
@@ -665,6 +690,7 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
     alloc(&e->ne_words, (size_t)NSLOT * n * 4ull * ((c->N + 3) / 4));
     alloc(&e->ne_first, (size_t)NSLOT * n * 4);
     alloc(&e->ne_legal, (size_t)NSLOT * n * 4ull * c->AW);
+    alloc(&e->ne_flags, (size_t)NSLOT * n * 4);
     alloc(&e->defer, n * 4);
     for (int p = 0; p < PF_LAG; ++p) {
         alloc(&e->pf_list[p], n * 4);
@@ -680,8 +706,6 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         if constexpr (K::CASCADE_LIMIT >= 0) alloc(&e->cont, RW * n * 4ull);
         return 0;
     });
-    // word 0 of every continuation record starts CONT_EMPTY (a record is ready once it holds a board index)
-    if (err == hipSuccess && e->cont) err = hipMemset(e->cont, 0xFF, n * 4ull);
     for (hipEvent_t& ev : e->gev)
         if (err == hipSuccess) err = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     // every per-board field starts zeroed: a never-reset env reads back zeros, not stale device memory
@@ -756,7 +780,7 @@ int m3_env_destroy(m3_env* e) {
     void* ptrs[] = {e->boards[0], e->boards[1], e->seeds, e->flags, e->draws, e->legal, e->score, e->moves,
                     e->next_action, e->reward, e->done, e->trunc, e->actions[0], e->actions[1], e->counters,
                     e->ovf_list,
-                    e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal,
+                    e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal, e->ne_flags,
                     e->spill, e->m397, e->cont, e->defer};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -805,8 +829,6 @@ int m3_env_reset(m3_env* e, const uint32_t* seeds, uint32_t seed_base) {
     HIP_TRY(hipMemsetAsync(e->counters, 0, 64 * 4 * MAX_SHARDS, c->stream));  // also clears the stats
     HIP_TRY(hipMemsetAsync(e->slot, 0, e->n, c->stream));
     e->steps = 0;
-    for (auto& sh : e->shards)
-        for (bool& z : sh.czero) z = true;  // (the memset above; the reset ends with a sync)
     int rc = with_shape(c->shape, [&](auto cf) {
         int r = launch_init<decltype(cf)>(c->stream, a, e->n);
         if (r == M3_OK && e->autoreset) r = fill_next_slots<decltype(cf)>(e);
@@ -1080,6 +1102,11 @@ int m3_env_stats(m3_env* e, uint64_t out[4]) {
 // profiling build only (not part of include/m3.h): out[2][PH_N + 2], summed over the
 // configurations' translation units (each has its own g_prof)
 #ifdef M3_SPLIT_TU
+#ifdef M3_HEADLINE_ONLY
+extern "C" int m3_prof_read_0(uint64_t*, int), m3_prof_read_1(uint64_t*, int);
+int m3_prof_read(uint64_t* out, int reset) {
+    int (*const rd[2])(uint64_t*, int) = {m3_prof_read_0, m3_prof_read_1};
+#else
 extern "C" int m3_prof_read_0(uint64_t*, int), m3_prof_read_1(uint64_t*, int), m3_prof_read_2(uint64_t*, int),
     m3_prof_read_3(uint64_t*, int), m3_prof_read_4(uint64_t*, int), m3_prof_read_5(uint64_t*, int),
     m3_prof_read_6(uint64_t*, int), m3_prof_read_7(uint64_t*, int), m3_prof_read_8(uint64_t*, int),
@@ -1089,6 +1116,7 @@ int m3_prof_read(uint64_t* out, int reset) {
     int (*const rd[10])(uint64_t*, int) = {m3_prof_read_0, m3_prof_read_1, m3_prof_read_2, m3_prof_read_3,
                                           m3_prof_read_4, m3_prof_read_5, m3_prof_read_6, m3_prof_read_7,
                                           m3_prof_read_8, m3_prof_read_9};
+#endif
     uint64_t part[2 * PROF_SLOTS];
     for (int i = 0; i < 2 * PROF_SLOTS; ++i) out[i] = 0;
     for (auto f : rd) {

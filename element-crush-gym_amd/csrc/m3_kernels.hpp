@@ -53,8 +53,12 @@ constexpr int FIX_GRID = 16;       // step fixup almost never has work: few bloc
 constexpr int INIT_FIX_BLOCK = 64;
 constexpr int INIT_BLOCK = 64;
 // active lanes of the one-board-per-lane fix / reset kernels (KS::BPW: one for the 32 x 32 frame)
+// (M3_WIDE_FRAME_LANES: an experiment knob, 64 to run the 32 x 32 frame one board per LANE again)
+#ifndef M3_WIDE_FRAME_LANES
+#define M3_WIDE_FRAME_LANES 1
+#endif
 template <class CF>
-constexpr uint32_t lanes_for() { return CF::W > 8 ? 1u : 64u; }
+constexpr uint32_t lanes_for() { return CF::W > 8 ? (uint32_t)M3_WIDE_FRAME_LANES : 64u; }
 // 9x9: k_init redoes its few >= 624-draw resets in-wave (wave_reset); 16x16
 // resets go straight to k_init_fix_lane (most need >= 624 draws)
 template <class CF>
@@ -92,7 +96,7 @@ struct KS {
     // ~2,500 SGPR spills through VGPR lanes, and with several lanes active some boards came out
     // wrong only in company (32x32x8 steps: 92 of 689; each exact alone) -- the lane interference
     // DESIGN.md §4 describes for the 16 x 16 frame. One active lane per wave has no divergence.
-    static constexpr int BPW = CF::W > 8 ? 1 : B;
+    static constexpr int BPW = CF::W > 8 ? M3_WIDE_FRAME_LANES : B;
 #ifndef M3_STEP_WPS
 #define M3_STEP_WPS 4
 #endif
@@ -116,20 +120,6 @@ struct KS {
 #define M3_CONT_WPS M3_STEP_WPS
 #endif
     static constexpr int CONT_WPS = CF::N > 128 ? 1 : M3_CONT_WPS;
-    // 1: k_env_step waves that finish their own boards take paused steps from the shard's queue
-    // (work-stealing tail, k_env_step phase 2); k_env_cont then only finishes the dead boards.
-    // 2: the same with a write-through hand-off (no fence). Off: both exact, both ~67 ms/step at
-    // 9x9x6 against 0.46 with the separate k_env_cont launch (gpurun_out/r04g, r04j)
-#ifndef M3_FUSED_CONT
-#define M3_FUSED_CONT 0
-#endif
-    // k_env_cont's persistent waves per shard launch (each loops over the paused-step queue)
-#ifndef M3_CONT_PERSIST
-#define M3_CONT_PERSIST 0
-#endif
-#ifndef M3_CONT_WAVES
-#define M3_CONT_WAVES 1024
-#endif
     // spill pool records per shard (32 x 32 frame: a record is 86 KB; fewer, the rest recompute)
     static constexpr uint32_t SPILL_RECORDS = CF::W > 8 ? 256 : 4096;
     // The env step's RNG is the register-only MT19937 chain from the board's
@@ -303,6 +293,13 @@ inline int m3_prof_read_tu(uint64_t* out, int reset) {
 }
 #endif
 
+// profiling build: wait for the wave's outstanding memory operations, so the next mark charges their
+// latency to the phase that issued them (no-op for every other Store)
+template <class S>
+__device__ __forceinline__ void prof_drain(S&) {
+    if constexpr (HasProf<S>::value) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 // Staging barrier of the one-wave (64-lane) workgroups: it only has to order
 // this wave's own LDS accesses (a wave's DS instructions execute in issue
 // order), so a wavefront-scope fence suffices. __syncthreads() would also make
@@ -318,6 +315,21 @@ __device__ __forceinline__ void lds_sync() {
 #else
     __syncthreads();
 #endif
+}
+
+// A step's counter block (8 words, EnvArgs::counters) is zeroed by the LAST kernel that reads it,
+// in place of a fill dispatch per shard-step: every block of that launch reads what it needs at
+// its start and takes a ticket (word 7) at its end; the block that draws the last ticket zeroes the
+// block, ticket included, for the step that reuses it PF_LAG steps later.
+__device__ __forceinline__ void zero_block_last(uint32_t* blk) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&blk[7], 1u) == gridDim.x - 1u) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) blk[i] = 0u;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -359,22 +371,6 @@ __device__ __forceinline__ bool block_copy_in_checked(const int8_t* __restrict__
 // zero-copy path of small host-buffer calls, where device atomics are not an option)
 __device__ __forceinline__ void flag_bad_cells(bool bad, uint32_t* flag) {
     if (flag && __any((int)bad) && __lane_id() == 0) *(volatile uint32_t*)flag = 1u;
-}
-
-// device-coherent word store / load (relaxed, agent scope: written through / read past the XCD's L2,
-// no cache-wide write-back or invalidate) -- the M3_FUSED_CONT=2 hand-off
-__device__ __forceinline__ void st_dev(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ uint32_t ld_dev(uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// block_copy_out through device-coherent stores (the block start is 4-byte aligned; tail bytes one by one)
-template <int BLOCK>
-__device__ __forceinline__ void block_copy_out_dev(int8_t* __restrict__ g, const uint8_t* lds, int bytes) {
-    const int n4 = bytes >> 2;
-    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(lds);
-    uint32_t* d4 = reinterpret_cast<uint32_t*>(g);
-    for (int i = threadIdx.x; i < n4; i += BLOCK) st_dev(d4 + i, s4[i]);
-    for (int i = (n4 << 2) + threadIdx.x; i < bytes; i += BLOCK)
-        __hip_atomic_store(reinterpret_cast<uint8_t*>(g) + i, lds[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int BLOCK>
@@ -627,11 +623,13 @@ struct InitArgs {
     uint8_t* done;
     uint8_t* trunc;
     uint32_t* flags;
+    uint32_t* slot_flags;        // nullable: M3_FLAG_RESET_CAP of the reset at ob (env episode slots), else 0
     uint32_t* stats;             // nullable: [0] resets, [1] reset recomputes (>= 624 draws)
     uint32_t* m397;              // nullable: mt[397] of the seed's init_genrand state at (slot, b)
     int64_t cstride;
     uint32_t* defer;             // nullable: items k_init leaves to k_init_coop (reset needs >= RESET_KCAP draws)
     uint32_t* defer_count;       // device count for defer (zeroed before k_init)
+    uint32_t* zero_at_end;       // nullable: the step's counter block; the chain's last kernel zeroes it
 };
 }  // namespace m3k
 using m3k::InitArgs;
@@ -694,6 +692,7 @@ __device__ __forceinline__ void init_outputs(const InitArgs& a, int64_t b, int64
     if (a.done) a.done[b] = 0;
     if (a.trunc) a.trunc[b] = 0;
     if (a.flags) a.flags[b] = fa < 0 ? FLAG_NO_LEGAL : 0u;
+    if (a.slot_flags) a.slot_flags[ob] = 0u;  // (k_init_fix_lane raises FLAG_RESET_CAP after this)
 }
 
 // Reset of board b on a tile stream generated in LDS (init_board_tiles).
@@ -923,6 +922,7 @@ __global__ void __launch_bounds__(64) k_init_coop(InitArgs a) {
         wave_reset<CF>(a, a.defer[q], key_s, cell_s, lane);
         if (a.stats && lane == 0) atomicAdd(&a.stats[1], 1u);
     }
+    if (a.zero_at_end) zero_block_last(a.zero_at_end);  // the env prefetch chain ends here (9x9)
 }
 
 // ---- lane-per-board reset for boards that need >= 624 draws -------------
@@ -1017,13 +1017,17 @@ __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
             }
             const int64_t ob = (int64_t)slot * a.sstride + b;
             init_outputs<CF>(a, b, ob, seed, m397, mt.draws(), P, dm);
-            if (rounds >= RESET_ROUND_CAP && a.flags) a.flags[b] |= FLAG_RESET_CAP;
+            if (rounds >= RESET_ROUND_CAP) {
+                if (a.flags) a.flags[b] |= FLAG_RESET_CAP;
+                if (a.slot_flags) a.slot_flags[ob] = FLAG_RESET_CAP;
+            }
             init_store_board<CF>(a, ob, P, dm);
             long_reset = mt.draws() >= 624u;
         }
         const uint64_t m = __ballot(long_reset);
         if (m && a.stats && (threadIdx.x & 63) == 0) atomicAdd(&a.stats[1], (uint32_t)__popcll(m));
     }
+    if (a.zero_at_end) zero_block_last(a.zero_at_end);  // the env prefetch chain ends here (16x16, frames)
 }
 
 // One round of randint(1, T+1, (R, C)) for a power-of-two T (every draw is a
@@ -1175,8 +1179,7 @@ struct EnvArgs {
     uint32_t* legal;  // nullable
     int32_t* packed;  // nullable: reward<<2 | trunc<<1 | done for the RCCL gather
     uint32_t* counters;  // this step's block: [0] overflow count, [1] prefetch count, [2] prefetch overflow
-                         // count, [3] spill records used, [4] continuation records, [5] records taken
-                         // (k_env_step phase 2 / persistent k_env_cont), [6] dead-board records
+                         // count, [3] spill records used, [4] continuation records
     uint32_t* spill;     // group-table spill pool of the shard
     uint32_t* stats;     // [0] step recomputes
     uint32_t* ovf_list;
@@ -1184,13 +1187,15 @@ struct EnvArgs {
     const uint32_t* ne_words;  // episode slots: initial cells (LE words) [3][n][NW]
     const int32_t* ne_first;   // [3][n] first seeded random action
     const uint32_t* ne_legal;  // [3][n][AW]
+    const uint32_t* ne_flags;  // [NSLOT][n] FLAG_RESET_CAP of the slot's reset (0 otherwise)
     uint32_t* pf_list;   // prefetch queue of this step: board, seed, slot
     uint32_t* pf_seed;
     uint32_t* pf_slot;
     const uint32_t* m397;  // [NSLOT][cstride] mt[397] of each slot's seed
     int64_t cstride;
-    uint32_t* cont;        // nullable: continuation records of paused steps (k_env_cont), [1 + WORDS][cont_stride]
+    uint32_t* cont;        // nullable: continuation records of paused steps (k_env_cont_grid), [1 + WORDS][cont_stride]
     int64_t cont_stride;
+    int zero_at_fix;       // k_env_fix zeroes the counter block (no prefetch chain reads it after the step)
 };
 }  // namespace m3k
 using m3k::EnvArgs;
@@ -1200,21 +1205,31 @@ namespace {
 // HL/VL of the resulting board), and the same-step autoreset (the finished
 // step's reward/done/flags stay visible, the observation and episode state
 // become the next episode's). mv / sc0: the board's moves and score before the
-// step. Returns false if the next random action ran past the RNG (recompute).
-// board_src (nullable): instead of loading the next episode's cells into P,
-// report their word row ob (ne_words[ob * NW ...]; -1 without a reset) so the
-// caller copies them once P is dead (k_env_step: keeps its register peak low).
+// step. Returns false if the next random action ran past the RNG (recompute);
+// nothing has been stored then.
+//
+// Memory order of the tail: every load it needs (the next episode's slot --
+// first action, legal set, cells -- and the lane's seed and slot) and the
+// prefetch-queue atomic are issued BEFORE its first store. A wave's vector
+// memory counter retires in issue order, so a load issued behind stores is
+// only usable once those stores are acknowledged too; written load / store /
+// load / store (the legal-set copy of the next episode), the wave paid one
+// full memory round trip per word (round-5 phase profile: 42 % of k_env_step's
+// wave cycles in this block, profiles/r05a_phase9.log).
+// row (nullable, k_env_step): the board's bytes go to this LDS staging row --
+// the resulting board, or the next episode's cells on a reset -- and P is not
+// needed afterwards. Without a row, P holds the board to write (the next
+// episode's on a reset).
 template <class CF, class RNG, class Store>
 __device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
                                            int r, uint32_t f, const typename CF::Bd& HL, const typename CF::Bd& VL,
-                                           int mv, int sc0, const typename CF::Dim& dm,
-                                           int64_t* board_src = nullptr) {
+                                           int mv, int sc0, const typename CF::Dim& dm, uint8_t* row = nullptr) {
     const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
     const int sc = sc0 + r;
     const int mv1 = mv + 1;
     const int tr = sc >= a.goal;                        // env.py:53
     const int dn = tr || mv1 == a.num_moves;            // env.py:54
-    a.draws[b] = stepped ? rng.draws() : 0u;
+    const uint32_t ndraws = stepped ? rng.draws() : 0u;  // the step's own draws (before the next action's)
     uint32_t act[CF::AW];
     action_bits<CF>(HL, VL, act, dm);
     int na = -1;
@@ -1224,57 +1239,93 @@ __device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a,
         if (na < 0) f |= FLAG_NO_LEGAL;
     }
     mark<PH_NEXT>(st);
+    const bool reset = dn && a.autoreset;
+    if (row) planes_to_bytes<CF>(P, row, dm);  // (LDS) P is dead from here on in k_env_step
+    mark<PH_TBYTES>(st);
+    // ---- loads: everything the stores below need ----
+    constexpr bool CELLS_IN_REGS = !CF::DYN;    // frame boards load their cells at the use
+    constexpr int NWS = (CF::N + 3) / 4;
+    const int NW = cell_words<CF>(dm);
+    const int AW = dm.aw();
+    uint32_t s_old = 0u, seed = 0u;
+    int64_t ob = 0;
+    int first = -1;
+    uint32_t nflags = 0u;  // the next episode's reset flags (FLAG_RESET_CAP)
+    uint32_t lg[CF::AW];
+    uint32_t cw[CELLS_IN_REGS ? NWS : 1];
+    if (reset) {  // swap in the prefetched next episode (slot + 1)
+        s_old = a.slot[b];
+        seed = a.seeds[b] + a.stride;
+        const uint32_t s_new = s_old + 1u == (uint32_t)NSLOT ? 0u : s_old + 1u;
+        ob = (int64_t)s_new * a.cstride + b;  // slots are strided by the env's n
+        first = a.ne_first[ob];
+        nflags = a.ne_flags ? a.ne_flags[ob] : 0u;
+        if (a.legal) {
+#pragma unroll
+            for (int i = 0; i < CF::AW; ++i) lg[i] = i < AW ? a.ne_legal[ob * AW + i] : 0u;
+        }
+        if constexpr (CELLS_IN_REGS) {
+#pragma unroll
+            for (int q = 0; q < NWS; ++q) cw[q] = a.ne_words[ob * NWS + q];
+        }
+        s_old = s_new;  // (from here on: the new slot)
+    }
+    prof_drain(st);
+    mark<PH_TLOAD>(st);
+    // the freed slot is queued for the episode after next: one atomic per wave, not per lane
+    const uint64_t m = __ballot(reset);
+    uint32_t qbase = 0u;
+    int leader = 0;
+    if (m) {
+        leader = __ffsll((unsigned long long)m) - 1;
+        if ((int)__lane_id() == leader) qbase = atomicAdd(&a.counters[1], (uint32_t)__popcll(m));
+    }
+    prof_drain(st);
+    mark<PH_TATOM>(st);
+    // ---- stores ----
+    a.draws[b] = ndraws;
     a.reward[b] = r;
     a.trunc[b] = (uint8_t)tr;
     a.done[b] = (uint8_t)dn;
-    a.flags[b] = f;
+    a.flags[b] = f | nflags;  // (a reset that stopped at its round cap flags the step that swapped it in)
     if (a.packed) a.packed[b] = (r << 2) | (tr << 1) | dn;
-    const bool reset = dn && a.autoreset;
     if (!reset) {
         a.score[b] = sc;
         a.moves[b] = mv1;
         a.next_action[b] = na;
-        if (a.legal) store_legal<CF>(a.legal + b * dm.aw(), act, dm);
-    } else {  // swap in the prefetched next episode (slot + 1)
-        const int NW = cell_words<CF>(dm);
-        const uint32_t s_old = a.slot[b], s_new = s_old + 1u == (uint32_t)NSLOT ? 0u : s_old + 1u;
-        const int64_t ob = (int64_t)s_new * a.cstride + b;  // slots are strided by the env's n
-        const uint32_t seed = a.seeds[b] + a.stride;
-        if (board_src) {
-            *board_src = ob;
-        } else if constexpr (CF::DYN) {
-            frame_from_bytes<CF>(reinterpret_cast<const uint8_t*>(a.ne_words + ob * NW), P, dm);
-        } else {
-            uint32_t cw[(CF::N + 3) / 4];
-#pragma unroll
-            for (int q = 0; q < NW; ++q) cw[q] = a.ne_words[ob * NW + q];
-            planes_from_words<CF>(cw, P);
-        }
-        a.slot[b] = (uint8_t)s_new;
+        if (a.legal) store_legal<CF>(a.legal + b * AW, act, dm);
+    } else {
+        a.slot[b] = (uint8_t)s_old;
         a.seeds[b] = seed;
         a.score[b] = 0;
         a.moves[b] = 0;
-        a.next_action[b] = a.ne_first[ob];
+        a.next_action[b] = first;
         if (a.legal) {
-            const int AW = dm.aw();
 #pragma unroll
             for (int i = 0; i < CF::AW; ++i)
-                if (i < AW) a.legal[b * AW + i] = a.ne_legal[ob * AW + i];
+                if (i < AW) a.legal[b * AW + i] = lg[i];
+        }
+        if constexpr (CELLS_IN_REGS) {
+            if (row) store_cells<CF::N>(row, cw);
+            else planes_from_words<CF>(cw, P);
+        } else {
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(a.ne_words + ob * NW);
+            if (row) {
+                for (int x = 0; x < dm.cells(); ++x) row[x] = src[x];
+            } else {
+                frame_from_bytes<CF>(src, P, dm);
+            }
         }
     }
     mark<PH_RESET>(st);
-    // queue the freed slot for the episode after next: one atomic per wave, not per lane
-    const uint64_t m = __ballot(reset);
     if (m) {
-        const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&a.counters[1], (uint32_t)__popcll(m));
-        base = __shfl(base, leader);
+        const int lane = (int)__lane_id();
+        qbase = __shfl(qbase, leader);
         if (reset) {
-            const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            const uint32_t q = qbase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
             a.pf_list[q] = (uint32_t)b;
-            a.pf_seed[q] = a.seeds[b] + (uint32_t)(NSLOT - 1) * a.stride;
-            a.pf_slot[q] = a.slot[b] == 0u ? (uint32_t)(NSLOT - 1) : a.slot[b] - 1u;
+            a.pf_seed[q] = seed + (uint32_t)(NSLOT - 1) * a.stride;
+            a.pf_slot[q] = s_old == 0u ? (uint32_t)(NSLOT - 1) : s_old - 1u;
         }
     }
     mark<PH_QUEUE>(st);
@@ -1290,12 +1341,12 @@ constexpr uint32_t FLAG_CONT_DEAD = 0x80u;
 // One Match3Env.step of board b. With DEFER (k_env_step), the cascade stops
 // after `limit` inner iterations and at a dead board (the shuffle path is left
 // out of the kernel): the step returns ENV_STEP_PAUSED with its state in P,
-// rng, r, f (f & FLAG_CONT_DEAD: dead) and has written nothing yet; k_env_cont
+// rng, r, f (f & FLAG_CONT_DEAD: dead) and has written nothing yet; k_env_cont_grid
 // finishes it. Without DEFER the whole step runs here.
 template <class CF, bool DEFER, class RNG, class Store>
 __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
                                             int limit, int& r, uint32_t& f, const typename CF::Dim& dm,
-                                            int64_t* board_src = nullptr) {
+                                            uint8_t* row = nullptr) {
     // every per-board input is loaded before the cascade, so its latency hides behind it
     const int act_in = a.actions ? a.actions[b] : a.next_action[b];
     const int mv = a.moves[b];
@@ -1312,7 +1363,7 @@ __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a
         }
     }
     if (f & FLAG_RECOMPUTE) return ENV_STEP_RECOMPUTE;
-    return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm, board_src) ? ENV_STEP_DONE
+    return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm, row) ? ENV_STEP_DONE
                                                                                    : ENV_STEP_RECOMPUTE;
 }
 
@@ -1323,102 +1374,12 @@ __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a
 template <class CF>
 using EnvCont = Cont<CF, typename KS<CF>::Rng>;
 
-// ---- work-stealing continuation (M3_FUSED_CONT) --------------------------
-// Record q of the queue is written as: every state word, then -- once the
-// writing wave's board stores are out -- (release) its board index in word 0,
-// so a wave taking q waits until word 0 is not CONT_EMPTY. Word 0 of every record is CONT_EMPTY between steps: the taker
-// (or k_env_cont, for the dead queue) restores it after reading.
-constexpr uint32_t CONT_EMPTY = 0xFFFFFFFFu;
-
-template <class CF, class RNG>
-__device__ __forceinline__ void cont_write(uint32_t* rec, int64_t cs, const typename CF::Bd* P, const RNG& rng, int r,
-                                           uint32_t f) {
-    if constexpr (M3_FUSED_CONT == 2) {
-        Cont<CF, RNG>::save(P, rng, r, f, [&](int i, uint32_t w) { st_dev(rec + (int64_t)(i + 1) * cs, w); });
-    } else {
-        Cont<CF, RNG>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
-    }
-}
-
-// a settled board with no legal move: the dead queue, from the top of the record area down
-template <class CF>
-__device__ __forceinline__ void cont_dead(const EnvArgs& a, int64_t b, const typename CF::Bd* P,
-                                          const typename KS<CF>::Rng& rng, int r, uint32_t f) {
-    const uint32_t qd = atomicAdd(&a.counters[6], 1u);
-    uint32_t* rec = a.cont + (a.n - 1 - (int64_t)qd);
-    cont_write<CF>(rec, a.cont_stride, P, rng, r, f | FLAG_CONT_DEAD);
-    rec[0] = (uint32_t)b;
-}
-
-// Phase 2 of k_env_step: take up to 64 queued records at a time (never past the
-// count reserved so far, so a record taken is one some running wave is writing)
-// and run each to its end -- the cascade unbounded, a board that settles dead
-// to the dead queue. A wave leaves when the queue is empty; a wave still in
-// phase 1 that queues more records comes here afterwards and takes them.
-template <class CF, class Store>
-__device__ __forceinline__ void env_steal(const EnvArgs& a, Store& st, const typename CF::Dim& dm) {
-    using K = KS<CF>;
-    const int t = threadIdx.x;
-    for (;;) {
-        uint32_t base = 0u, k = 0u;
-        if (t == 0) {
-            for (;;) {
-                const uint32_t T = __hip_atomic_load(&a.counters[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t R = __hip_atomic_load(&a.counters[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (T >= R) break;
-                const uint32_t want = R - T < 64u ? R - T : 64u;
-                if (atomicCAS(&a.counters[5], T, T + want) == T) {
-                    base = T;
-                    k = want;
-                    break;
-                }
-            }
-        }
-        base = __shfl(base, 0);
-        k = __shfl(k, 0);
-        if (k == 0u) break;
-        if ((uint32_t)t < k) {
-            uint32_t* rec = a.cont + base + t;
-            uint32_t bw;
-            if constexpr (M3_FUSED_CONT == 2) {
-                while ((bw = ld_dev(rec)) == CONT_EMPTY) __builtin_amdgcn_s_sleep(2);
-            } else {
-                while ((bw = __hip_atomic_load(rec, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == CONT_EMPTY)
-                    __builtin_amdgcn_s_sleep(2);
-            }
-            const int64_t b = bw;
-            const int64_t cs = a.cont_stride;
-            typename CF::Bd P[CF::NP], HL, VL;
-            typename K::Rng rng;
-            int r;
-            uint32_t f;
-            EnvCont<CF>::load(P, rng, r, f, [&](int i) {
-                return M3_FUSED_CONT == 2 ? ld_dev(rec + (int64_t)(i + 1) * cs) : rec[(int64_t)(i + 1) * cs];
-            });
-            rec[0] = CONT_EMPTY;
-            const int mv = a.moves[b], sc0 = a.score[b];
-            const int c = apply_cascade_ex<CF, CASX_STOP_DEAD>(P, rng, f, HL, VL, st, r, -1, false, dm);
-            if (c == CAS_DEAD && !(f & FLAG_RECOMPUTE)) {
-                cont_dead<CF>(a, b, P, rng, r, f);
-            } else {
-                const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm);
-                if (!ok) {
-                    const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-                    a.ovf_list[slot] = (uint32_t)b;
-                } else {
-                    planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
-                }
-            }
-        }
-    }
-}
-
 template <class CF>
 __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArgs a) {
     // The board staging area is only live before the cascade (HBM -> LDS ->
     // planes) and after it (planes -> LDS -> HBM), the match-group table only
     // inside it; with one wave per workgroup nothing else can touch the LDS
-    // in between, so the two share storage (13.3 KB per wave at 9x9: 3 waves/SIMD).
+    // in between, so the two share storage (6 KB per wave at 9x9).
     using K = KS<CF>;
     static_assert(K::B == 64, "staging/table aliasing assumes one wave per workgroup");
     constexpr int STAGE_WORDS = (K::B * CF::N + 16 + 3) / 4;
@@ -1447,115 +1408,57 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     st.spill = a.spill;
     st.pool_next = &a.counters[3];
     st.pool_cap = K::SPILL_RECORDS;
-    uint32_t pub_q = ~0u, pub_b = 0u;  // this lane's queued record (M3_FUSED_CONT), marked ready at the end
     if (t < nb) {
         const int64_t b = b0 + t;
         typename CF::Bd P[CF::NP];
-        lds_to_planes<CF>(lds, t, P, dm);
+        lds_to_planes<CF>(lds, t, P, dm);  // (every lane of the wave, before any group-table write)
         typename K::Rng rng;
         rng.init(a.seeds[b], a.m397[(int64_t)cslot * a.cstride + b]);
         int r;
         uint32_t f;
         int res;
-        int64_t reset_src = -1;  // autoreset: the next episode's cells, copied below once P is dead
+        // a finished step leaves its board bytes (or the next episode's) in its staging row
+        uint8_t* const row = lds + t * NC;
         if constexpr (K::CASCADE_LIMIT >= 0)  // (a.cont is set)
-            res = env_step_one<CF, true>(P, a, b, rng, st, K::CASCADE_LIMIT, r, f, dm, &reset_src);
+            res = env_step_one<CF, true>(P, a, b, rng, st, K::CASCADE_LIMIT, r, f, dm, row);
         else
-            res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f, dm, &reset_src);
-        if (res == ENV_STEP_RECOMPUTE) {
+            res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f, dm, row);
+        if (res == ENV_STEP_RECOMPUTE) {  // (its row is rewritten by k_env_fix)
             const uint32_t slot = atomicAdd(&a.counters[0], 1u);
             a.ovf_list[slot] = (uint32_t)b;
         }
-        // paused steps leave a continuation record (one atomic per wave)
+        // paused steps leave a continuation record (one atomic per wave); their rows are
+        // rewritten by k_env_cont_grid
         const bool paused = res == ENV_STEP_PAUSED;
-        if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT) {
-            // cascades past the bound join the shard's queue (phase 2 below takes them); boards that
-            // settled dead go to the dead queue at the top of the record area (k_env_cont, after).
-            // A queued record is only marked ready after this wave's board stores below: its board
-            // slot in nxt holds stale bytes until the record's taker writes the finished board.
-            const bool dead = paused && (f & FLAG_CONT_DEAD);
-            const bool cont = paused && !dead;
-            const uint64_t m = __ballot(cont);
-            if (m) {
-                const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
-                base = __shfl(base, leader);
-                if (cont) {
-                    pub_q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                    pub_b = (uint32_t)b;
-                    cont_write<CF>(a.cont + pub_q, a.cont_stride, P, rng, r, f);
-                }
-            }
-            if (dead) cont_dead<CF>(a, b, P, rng, r, f);
-        } else {
-            const uint64_t m = K::CASCADE_LIMIT >= 0 ? __ballot(paused) : 0ull;
-            if (m) {
-                const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
-                base = __shfl(base, leader);
-                if (paused) {
-                    const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                    uint32_t* rec = a.cont + q;
-                    const int64_t cs = a.cont_stride;
-                    rec[0] = (uint32_t)b;
-                    EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
-                }
-            }
-        }
-        planes_to_bytes<CF>(P, lds + t * NC, dm);  // a paused board's bytes are rewritten by k_env_cont
-        if (reset_src >= 0) {
-            if constexpr (CF::DYN) {
-                const uint8_t* src = reinterpret_cast<const uint8_t*>(a.ne_words + reset_src * cell_words<CF>(dm));
-                for (int x = 0; x < NC; ++x) lds[t * NC + x] = src[x];
-            } else {
-                constexpr int NW = (CF::N + 3) / 4;
-                uint32_t cw[NW];
-#pragma unroll
-                for (int q = 0; q < NW; ++q) cw[q] = a.ne_words[reset_src * NW + q];
-                store_cells<CF::N>(lds + t * CF::N, cw);
+        const uint64_t m = K::CASCADE_LIMIT >= 0 ? __ballot(paused) : 0ull;
+        if (m) {
+            const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (paused) {
+                const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                uint32_t* rec = a.cont + q;
+                const int64_t cs = a.cont_stride;
+                rec[0] = (uint32_t)b;
+                EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
             }
         }
     }
     lds_sync();
-    if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT == 2) {
-        // boards and records written through (device-coherent stores), waited for, then the record
-        // is marked ready: no cache-wide maintenance, and a stolen board's final bytes (the stealer's
-        // ordinary stores) land after the owner's copy
-        block_copy_out_dev<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
-        __builtin_amdgcn_s_waitcnt(0);
-        if (pub_q != ~0u) st_dev(a.cont + pub_q, pub_b);
-    } else {
-        block_copy_out<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
-    }
-    if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT == 1) {
-        if (pub_q != ~0u) {  // the board stores above are visible before the record is marked ready
-            __threadfence();
-            __hip_atomic_store(a.cont + pub_q, pub_b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if constexpr (K::CASCADE_LIMIT >= 0 && M3_FUSED_CONT) {
-        lds_sync();  // the group table reuses the staging area
-        env_steal<CF>(a, st, dm);
-    }
+    block_copy_out<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
 #ifdef M3_PHASE_PROF
     if (live) st.end(0);
 #endif
 }
 
 // Finish the steps k_env_step paused (their cascade ran past KS::CASCADE_LIMIT
-// inner iterations, or it settled on a board with no legal move). The paused
-// boards are the long cascades of a launch, and their remaining iteration
-// counts still differ a lot: a wave that took 64 of them and ran each to the
-// end would run as long as its longest. Instead every lane advances its board
-// by ONE cascade iteration per trip (apply_cascade_ex with limit 1) and, when
-// that board is finished (bookkeeping + board written straight to nxt), takes
-// the next record from the launch's queue (one wave-aggregated atomic per trip
-// that needs records, counter block [5]), so the waves stay full until the
-// queue drains. Persistent grid: a fixed number of waves loops over the records.
+// inner iterations, or it settled on a board with no legal move: the row
+// shuffle): the long cascades of a launch, packed densely into waves instead
+// of holding every lane of their k_env_step wave idle. Grid-stride over the
+// records; each board is written straight to nxt.
 template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont(EnvArgs a) {
+__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont_grid(EnvArgs a) {
     using K = KS<CF>;
     // The few waves of this kernel are the step's critical path; they share SIMDs with
     // the other shard's step waves and the resets: issue first (A/B: within noise).
@@ -1567,77 +1470,9 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont(EnvArg
     st.pool_next = &a.counters[3];
     st.pool_cap = K::SPILL_RECORDS;
     const int64_t cs = a.cont_stride;
-    const typename CF::Dim dm(a.shape);
-    const int lane = (int)__lane_id();
-    typename CF::Bd P[CF::NP], HL, VL;
-    typename K::Rng rng;
-    int r = 0;
-    uint32_t f = 0u;
-    int64_t b = -1;        // this lane's board (-1: none)
-    bool settled = false;  // its next trip starts at the legal set (a dead board: the shuffle)
-    bool exhausted = false;
-    for (;;) {
-        const bool need = b < 0 && !exhausted;
-        const uint64_t nm = __ballot(need);
-        if (nm) {  // lanes without a board take the next records
-            const int leader = __ffsll((unsigned long long)nm) - 1;
-            uint32_t base = 0u;
-            if (lane == leader) base = atomicAdd(&a.counters[5], (uint32_t)__popcll(nm));
-            base = __shfl(base, leader);
-            if (need) {
-                const uint32_t q = base + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
-                if (q < cnt) {
-                    const uint32_t* rec = a.cont + q;
-                    b = rec[0];
-                    EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
-                    settled = (f & FLAG_CONT_DEAD) != 0;  // settled with no legal move: continue at the shuffle
-                    f &= ~FLAG_CONT_DEAD;
-                } else {
-                    exhausted = true;
-                }
-            }
-        }
-        if (!__any(b >= 0)) break;
-        if (b >= 0) {
-            const int c = apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, 1, settled, dm);
-            settled = false;
-            if (c != CAS_PAUSED) {  // finished (or flagged for the exact recompute)
-                const int mv = a.moves[b], sc0 = a.score[b];
-                const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm);
-                if (!ok) {
-                    const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-                    a.ovf_list[slot] = (uint32_t)b;
-                } else {
-                    planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
-                }
-                b = -1;
-            }
-        }
-    }
-}
-
-// (M3_CONT_PERSIST=0) One paused step per lane, each run to its end.
-// Finish the steps k_env_step paused (their cascade ran past KS::CASCADE_LIMIT
-// inner iterations): the long cascades of a launch, packed densely into waves
-// instead of holding every lane of their k_env_step wave idle. Grid-stride
-// over the records; each board is written straight to nxt.
-template <class CF>
-__global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont_grid(EnvArgs a) {
-    using K = KS<CF>;
-    // The few waves of this kernel are the step's critical path; they share SIMDs with
-    // the other shard's step waves and the resets: issue first (A/B: within noise).
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
-    const uint32_t cnt = M3_FUSED_CONT ? a.counters[6] : a.counters[4];  // (fused: the dead queue only)
-    LdsStore<CF, K::GCAP, K::B> st{as_lds(tab + threadIdx.x)};
-    st.spill = a.spill;
-    st.pool_next = &a.counters[3];
-    st.pool_cap = K::SPILL_RECORDS;
-    const int64_t cs = a.cont_stride;
     for (uint32_t q = blockIdx.x * K::B + threadIdx.x; q < cnt; q += gridDim.x * K::B) {
-        uint32_t* rec = a.cont + (M3_FUSED_CONT ? a.n - 1 - (int64_t)q : (int64_t)q);
+        const uint32_t* rec = a.cont + q;
         const int64_t b = rec[0];
-        if (M3_FUSED_CONT) rec[0] = CONT_EMPTY;
         typename CF::Bd P[CF::NP];
         typename K::Rng rng;
         int r;
@@ -1690,6 +1525,7 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
         }
         planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
     }
+    if (a.zero_at_fix) zero_block_last(a.counters);
 }
 
 // ---------------------------------------------------------------------------
@@ -1915,8 +1751,9 @@ struct m3_env {
     uint32_t* ne_words = nullptr;
     int32_t* ne_first = nullptr;
     uint32_t* ne_legal = nullptr;
+    uint32_t* ne_flags = nullptr;  // [NSLOT][n] M3_FLAG_RESET_CAP of each slot's reset
     uint32_t* m397 = nullptr;  // [NSLOT][n]
-    uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont)
+    uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont_grid)
     uint32_t* defer = nullptr; // prefetch resets k_init leaves to k_init_coop [n]
     // prefetch queues and their overflow lists, by step % PF_LAG
     uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {};
@@ -1940,9 +1777,6 @@ struct m3_env {
         bool apending[2] = {};
         hipEvent_t pev[PF_LAG] = {};   // prefetch of queue q done
         bool ppending[PF_LAG] = {};
-        // counter block q already zeroed for its next step: by the reset, or on the
-        // prefetch stream after its last reader (ordered before that step by pev[q])
-        bool czero[PF_LAG] = {};
     };
     std::vector<Shard> shards;
     // `packed` is double-buffered by step parity, so the RCCL gather of step t
@@ -2030,6 +1864,7 @@ void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
     r.first_action = e->ne_first + o;
     r.legal = e->ne_legal + o * e->ctx->AW;
     r.m397 = e->m397 + o;
+    r.slot_flags = e->ne_flags + o;
     r.cstride = e->n;
 }
 
@@ -2086,6 +1921,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.ne_words = e->ne_words + o * ((N + 3) / 4);
     a.ne_first = e->ne_first + o;
     a.ne_legal = e->ne_legal + o * AW;
+    a.ne_flags = e->ne_flags + o;
     a.pf_list = e->pf_list[par] + o;
     a.pf_seed = e->pf_seed[par] + o;
     a.pf_slot = e->pf_slot[par] + o;
@@ -2093,26 +1929,15 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.cstride = e->n;
     a.cont = KS<CF>::CASCADE_LIMIT >= 0 ? e->cont + o : nullptr;
     a.cont_stride = e->n;
-    if (!sh.czero[par]) HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), st));
-    sh.czero[par] = false;
+    a.zero_at_fix = !e->autoreset;  // (with autoreset the prefetch chain is the block's last reader)
     const bool timed = e->tn < e->tcap;
     if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], st));
     hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
     HIP_TRY(hipGetLastError());
     if constexpr (KS<CF>::CASCADE_LIMIT >= 0) {
-#if M3_CONT_PERSIST
-        // persistent waves over the device-side queue of paused steps (~19 % of the boards at limit 2)
-        int64_t g = ((int64_t)(sh.n * 0.2) + KS<CF>::B - 1) / KS<CF>::B;
-        g = g < 1 ? 1 : (g > M3_CONT_WAVES ? M3_CONT_WAVES : g);
-        hipLaunchKernelGGL(k_env_cont<CF>, dim3((unsigned)g), dim3(KS<CF>::B), 0, st, a);
-#elif M3_FUSED_CONT
-        // the dead boards left by k_env_step's phases (~1e-5 of the steps): a few blocks, grid-strided
-        hipLaunchKernelGGL(k_env_cont_grid<CF>, dim3(FIX_GRID), dim3(KS<CF>::B), 0, st, a);
-#else
         // grid-strides over the device-side count of paused steps: sized for their usual share (~20 % at limit 2)
         const int64_t g = ((int64_t)(sh.n * 0.25) + KS<CF>::B - 1) / KS<CF>::B;
         hipLaunchKernelGGL(k_env_cont_grid<CF>, dim3((unsigned)(g > 0 ? g : 1)), dim3(KS<CF>::B), 0, st, a);
-#endif
         HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(k_env_fix<CF>, dim3(fix_grid<CF>()), dim3(FIX_BLOCK), 0, st, a);
@@ -2135,6 +1960,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.list_slot = e->pf_slot[par] + o;
         r.list_count = &cnt[1];
         r.stats = base + 41;
+        r.zero_at_end = cnt;  // the chain's last kernel zeroes this step's counter block
         if constexpr (INIT_INLINE_FIX<CF> || (!CF::DYN && M3_RESET16_CHAIN2)) {
             r.defer = e->defer + o;
             r.defer_count = &cnt[2];  // zeroed with the block
@@ -2145,11 +1971,8 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         int rc = launch_init<CF>(sh.pstream, r, sh.n / 8 + 1);
         if (rc) return rc;
 #endif
-        // the resets were the block's last readers: zero it here, off the step's critical path
-        HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), sh.pstream));
         HIP_TRY(hipEventRecord(sh.pev[par], sh.pstream));
         sh.ppending[par] = true;
-        sh.czero[par] = true;
     }
     return M3_OK;
 }
@@ -2203,8 +2026,6 @@ int rederive(m3_env* e) {
     if (rc) return rc;
     e->steps = 0;
     e->gpend[0] = e->gpend[1] = false;
-    for (auto& sh : e->shards)
-        for (bool& z : sh.czero) z = true;  // (the memset above; this ends with a sync)
     if (e->autoreset) {
         rc = fill_next_slots<CF>(e);
         if (rc) return rc;

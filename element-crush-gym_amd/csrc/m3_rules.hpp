@@ -28,7 +28,7 @@ namespace m3 {
 // phase boundaries (m3_api.hip builds such a variant with -DM3_PHASE_PROF);
 // for every other Store the calls compile to nothing.
 enum : int { PH_LOAD, PH_SWAP, PH_MATCH, PH_CLEAR, PH_DROP, PH_REFILL, PH_LEGAL, PH_NEXT, PH_RESET, PH_QUEUE,
-             PH_STORE, PH_N };
+             PH_STORE, PH_TBYTES, PH_TLOAD, PH_TATOM, PH_N };
 template <class S, class = void>
 struct HasProf : std::false_type {};
 template <class S>
@@ -272,6 +272,22 @@ struct FrameDim {
     M3_HD uint32_t tile_mask() const { return tmask; }
     M3_HD Bd valid() const { return vmask; }
 };
+
+// wave-wide "any" (host build: the lane itself)
+M3_HD bool wave_any(bool p) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __any((int)p) != 0;
+#else
+    return p;
+#endif
+}
+
+// The cascade loop of apply_cascade_ex with a wave-uniform exit (see there): 1 everywhere, 2 in the
+// frame configurations only (the specialised 16x16x8 step measured 9 % slower with it, 9x9 1-2 %),
+// 0 nowhere
+#ifndef M3_UNIFORM_CASCADE
+#define M3_UNIFORM_CASCADE 2
+#endif
 
 // boards of at least this many words take the word-sliced legal_masks (0: never)
 #ifndef M3_LEGAL_SLICED_W
@@ -903,8 +919,62 @@ M3_HD void merge_clip(typename CF::Bd* P, const typename CF::Bd& z, const typena
 // gravity + refill (:166-173). Columns left to right, new tiles on top in draw
 // order (new[0] at row 0). Tiles come from randint(1, T+1).
 // gravity: returns the (top-aligned) empty cells
+//
+// Round 5: by the binary decomposition of every tile's drop distance (the number of holes below
+// it in its column), low bits first -- stage i moves the tiles whose distance has bit i set by
+// 2^i rows. This is Hacker's Delight's `compress` (7-4) run down every column at once: the bit i
+// of each distance is a column-wise suffix parity of the holes still counted (mp), and moving
+// the low bits first never lets two tiles meet. A stage no lane of the wave needs is skipped as
+// a whole (wave-uniform branch): the wave runs ceil(log2 R) fixed stages at most instead of the
+// row-by-row loop's max-drop + 1 passes, with no divergence (M3_GRAVITY_LOOP=1: the loop).
+#ifndef M3_GRAVITY_LOOP
+#define M3_GRAVITY_LOOP 0
+#endif
+template <class CF>
+M3_HD typename CF::Bd gravity_decomp(typename CF::Bd* P, const typename CF::Dim& dm = typename CF::Dim{}) {
+    using Bd = typename CF::Bd;
+    constexpr int C = CF::C, R = CF::R, NPU = 6;
+    constexpr int STAGES = ceil_log2(R);           // drop distances < R
+    const Bd VALID = dm.valid();                   // walls are neither holes nor tiles
+    Bd m = P[0];
+#pragma unroll
+    for (int p = 1; p < NPU; ++p) m |= P[p];
+    Bd mk = at<C>(VALID.andnot(m));                // a hole right below
+    auto stage = [&](auto S) {
+        constexpr int D = (1 << decltype(S)::value) * C;  // rows moved in this stage, as bits
+        Bd mp = mk ^ at<C>(mk);                    // holes below, counted mod 2 down the column
+        if constexpr (R > 3) mp ^= at<2 * C>(mp);  // (a suffix over the R - 1 cells below)
+        if constexpr (R > 5) mp ^= at<4 * C>(mp);
+        if constexpr (R > 9) mp ^= at<8 * C>(mp);
+        if constexpr (R > 17) mp ^= at<16 * C>(mp);
+        const Bd mv = mp & m;                      // tiles whose distance has this bit
+        if (wave_any(mv.any())) {
+            m = m.andnot(mv) | at<-D>(mv);
+#pragma unroll
+            for (int p = 0; p < NPU; ++p) {
+                const Bd t = P[p] & mv;
+                P[p] = P[p].andnot(mv) | at<-D>(t);
+            }
+        }
+        mk = mk.andnot(mp);
+    };
+    stage(std::integral_constant<int, 0>{});
+    if constexpr (STAGES > 1) if (wave_any(mk.any())) {
+        stage(std::integral_constant<int, 1>{});
+        if constexpr (STAGES > 2) if (wave_any(mk.any())) {
+            stage(std::integral_constant<int, 2>{});
+            if constexpr (STAGES > 3) if (wave_any(mk.any())) {
+                stage(std::integral_constant<int, 3>{});
+                if constexpr (STAGES > 4) if (wave_any(mk.any())) stage(std::integral_constant<int, 4>{});
+            }
+        }
+    }
+    return VALID.andnot(m);
+}
+
 template <class CF>
 M3_HD typename CF::Bd gravity(typename CF::Bd* P, const typename CF::Dim& dm = typename CF::Dim{}) {
+    if constexpr (!M3_GRAVITY_LOOP) return gravity_decomp<CF>(P, dm);
     using Bd = typename CF::Bd;
     constexpr int C = CF::C, R = CF::R, NPU = 6;
     const Bd VALID = dm.valid();  // walls are neither holes nor tiles
@@ -1155,6 +1225,59 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
         Bd mask;
         bool found = false;
         if (!settled) {
+            if constexpr (M3_UNIFORM_CASCADE == 1 || (M3_UNIFORM_CASCADE == 2 && CF::DYN)) {
+                // cascade: refill, rematch, clear while matches remain -- with a wave-UNIFORM loop exit:
+                // the wave runs its longest lane's trip count (as the divergent loop does) with the
+                // body predicated per lane, so no value leaves the loop from a lane that quit early.
+                // Values live out of a divergent loop came back stale (or garbage) for such lanes
+                // whenever the kernel spilled VGPRs (the frame-kernel lane
+                // interference; tools/dbg/lanes*.py).
+                int xr = -1;  // an early return (paused, group overflow)
+                bool live = true;
+                for (;;) {
+                    if (!wave_any(live)) break;
+                    if (!live) continue;
+                    if (it == limit) {                              // paused before iteration limit + 1
+                        xr = CAS_PAUSED;
+                        live = false;
+                        continue;
+                    }
+                    if constexpr (CF::DYN || !DrawBounded<RNG>::value) {
+                        if (it >= CASCADE_CAP) {
+                            flags |= FLAG_CASCADE_CAP;
+                            live = false;
+                            continue;
+                        }
+                    }
+                    ++it;
+                    const Bd em = gravity<CF>(P, dm);               // :166-173
+                    mark<PH_DROP>(st);
+                    refill<CF>(P, em, rng, dm);
+                    mark<PH_REFILL>(st);
+                    if (rng.overflow) {
+                        live = false;
+                        continue;
+                    }
+                    const int mr = get_matches<CF>(P, mask, sw, st);  // :176-181
+                    mark<PH_MATCH>(st);
+                    if (mr == MATCH_OVERFLOW) {
+                        flags |= FLAG_GROUP_OVERFLOW;
+                        xr = CAS_DONE;
+                        live = false;
+                        continue;
+                    }
+                    if (mr != MATCH_FOUND) {
+                        live = false;
+                        continue;
+                    }
+                    Bd z = mask | VALID.andnot(tb_nonzero<CF>(P));  // :199 + TB==0 cells
+                    z = fire_specials<CF, 6>(P, z, dm);
+                    reward += score<CF, 6>(P, z);
+                    merge_clip<CF, 6>(P, z, sw);
+                    mark<PH_CLEAR>(st);
+                }
+                if (xr >= 0) return xr;
+            } else {
             for (;;) {  // cascade: refill, rematch, clear while matches remain
                 if (it == limit) return CAS_PAUSED;             // paused before iteration limit + 1
                 if constexpr (CF::DYN || !DrawBounded<RNG>::value) {
@@ -1181,6 +1304,7 @@ M3_HD int apply_cascade_ex(typename CF::Bd* P, RNG& rng, uint32_t& flags, typena
                 reward += score<CF, 6>(P, z);
                 merge_clip<CF, 6>(P, z, sw);
                 mark<PH_CLEAR>(st);
+            }
             }
             if (rng.overflow) break;
             if constexpr ((OPTS & CASX_STOP_SETTLED) != 0) return CAS_SETTLED;
@@ -1342,14 +1466,6 @@ struct TileGen {
     static constexpr int MAXR = 624 / CF::N + 2;  // rounds one MT block can feed
 };
 
-// wave-wide "any": the stream below is generated in wave-uniform chunks
-M3_HD bool wave_any(bool p) {
-#ifdef __HIP_DEVICE_COMPILE__
-    return __any((int)p) != 0;
-#else
-    return p;
-#endif
-}
 
 template <class CF, class RNG, class RawSink, class AccSink, class S = NoStore>
 M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* pos, int stride, uint32_t& draws,

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("M3_LIB", os.path.join(_PKG_ROOT, "build", "libm3.so")
 
 M3_OK = 0
 ERR_NAMES = {-1: "M3_ERR_INVALID", -2: "M3_ERR_UNSUPPORTED", -3: "M3_ERR_HIP", -4: "M3_ERR_RCCL",
-             -5: "M3_ERR_NO_DEVICE", -6: "M3_ERR_STATE"}
+             -5: "M3_ERR_NO_DEVICE", -6: "M3_ERR_STATE", -7: "M3_ERR_CAP"}
 
 FLAG_TERMINAL = 0x01
 FLAG_BAD_ACTION = 0x02
@@ -34,7 +34,7 @@ ENV_BOARDS, ENV_REWARD, ENV_DONE, ENV_TRUNCATED, ENV_SCORE, ENV_MOVES, ENV_FLAGS
 EXPORTS = [
     "m3_abi_version", "m3_last_error", "m3_device_count", "m3_supported", "m3_action_space",
     "m3_ctx_create", "m3_ctx_destroy", "m3_ctx_synchronize", "m3_dev_alloc", "m3_dev_free", "m3_dev_copy",
-    "m3_init_boards", "m3_apply_actions", "m3_legal_actions", "m3_rollouts", "m3_rollouts_device",
+    "m3_init_boards", "m3_init_boards_ex", "m3_apply_actions", "m3_legal_actions", "m3_rollouts", "m3_rollouts_device",
     "m3_env_create", "m3_env_destroy", "m3_env_reset", "m3_env_set_shards", "m3_env_synchronize",
     "m3_env_set_autoreset", "m3_env_step",
     "m3_env_step_device", "m3_env_get", "m3_env_set", "m3_env_device_ptr",
@@ -80,6 +80,7 @@ def lib():
             "m3_dev_free": ([vp, vp], i32),
             "m3_dev_copy": ([vp, vp, vp, i64, i32], i32),
             "m3_init_boards": ([vp, i64, vp, vp, vp, vp], i32),
+            "m3_init_boards_ex": ([vp, i64, vp, vp, vp, vp, vp], i32),
             "m3_apply_actions": ([vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
             "m3_legal_actions": ([vp, i64, vp, vp], i32),
             "m3_rollouts": ([vp, i64] + [vp] * 9, i32),
@@ -205,15 +206,22 @@ class Context:
             raise ValueError("cell values must lie in [0, 127]")
         return np.ascontiguousarray(b.reshape(-1, self.N), dtype=np.int8)
 
-    def init_boards(self, seeds):
+    def init_boards(self, seeds, flags=False):
+        """BoardV2.__init__ of each seed: (boards, draws, first_action[, flags]). Without flags, a reset
+        that stopped at the redraw-round cap raises (M3_ERR_CAP: the reference would keep drawing)."""
         seeds = np.ascontiguousarray(np.atleast_1d(seeds), dtype=np.uint32)
         n = len(seeds)
         out = np.empty((n, self.N), np.int8)
         draws = np.empty(n, np.uint32)
         first = np.empty(n, np.int32)
+        fl = np.empty(n, np.uint32) if flags else None
         with self._lock:
-            check(lib().m3_init_boards(self.handle, n, ptr(seeds), ptr(out), ptr(draws), ptr(first)))
-        return out.reshape(n, self.rows, self.columns), draws, first
+            if flags:
+                check(lib().m3_init_boards_ex(self.handle, n, ptr(seeds), ptr(out), ptr(draws), ptr(first), ptr(fl)))
+            else:
+                check(lib().m3_init_boards(self.handle, n, ptr(seeds), ptr(out), ptr(draws), ptr(first)))
+        res = (out.reshape(n, self.rows, self.columns), draws, first)
+        return res + (fl,) if flags else res
 
     def apply_actions(self, boards, seeds, n_actions, actions, legal=False, next_action=False):
         b = self._boards(boards)

@@ -70,11 +70,16 @@ def max_over_ranks(value: float, dist=None) -> float:
     return float(t.item())
 
 
-def timed_steps(step, sync, steps: int, warmup: int, dist=None, on_start=None) -> float:
+def timed_steps(step, sync, steps: int, warmup: int, dist=None, on_start=None, on_end=None,
+                return_local: bool = False):
     """Run `warmup` untimed then exactly `steps` timed calls of step(); seconds, max over ranks.
 
     on_start() runs after the opening barrier, just before the clock starts
-    (bench.py arms the per-launch HIP event timing there)."""
+    (bench.py arms the per-launch HIP event timing there); on_end() runs after
+    the last timed step and before the closing device sync, so whatever it
+    enqueues is timed (bench.py --gather final: the one RCCL all-gather of the
+    last step's outcome words). With return_local, returns (max over ranks,
+    this rank's own seconds)."""
     for _ in range(warmup):
         step()
     sync()
@@ -85,8 +90,11 @@ def timed_steps(step, sync, steps: int, warmup: int, dist=None, on_start=None) -
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    if on_end is not None:
+        on_end()
     sync()
     elapsed = time.perf_counter() - t0
     if _active(dist):
         dist.barrier()
-    return max_over_ranks(elapsed, dist)
+    mx = max_over_ranks(elapsed, dist)
+    return (mx, elapsed) if return_local else mx

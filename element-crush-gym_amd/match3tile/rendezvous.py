@@ -30,6 +30,14 @@ import threading
 import time
 
 _HDR = struct.Struct("<I")
+_ERR = 0xFFFFFFFF  # round header of an error frame: the server failed, the text follows
+
+
+def default_timeout():
+    """Seconds a socket waits for a peer (M3_RDV_TIMEOUT; 0 = forever). Long by default: the ranks
+    may build the library one after another between two rounds."""
+    v = float(os.environ.get("M3_RDV_TIMEOUT", "3600"))
+    return None if v <= 0 else v
 
 
 def _send(sock, data: bytes):
@@ -54,9 +62,9 @@ def _recv(sock) -> bytes:
 class RendezvousServer:
     """Accepts `world` ranks, then serves allgather rounds until every rank has disconnected."""
 
-    def __init__(self, world: int, host: str = "127.0.0.1", port: int = 0, timeout: float = 600.0):
+    def __init__(self, world: int, host: str = "127.0.0.1", port: int = 0, timeout: float = -1.0):
         self.world = world
-        self.timeout = timeout
+        self.timeout = default_timeout() if timeout is not None and timeout < 0 else timeout
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self.sock.bind((host, port))
@@ -91,8 +99,15 @@ class RendezvousServer:
                 out = _HDR.pack(self.world) + b"".join(_HDR.pack(len(f)) + f for f in frames)
                 for c in conns:
                     _send(c, out)
-        except Exception as e:  # surfaced to the clients as a closed connection
+        except Exception as e:  # surfaced to the clients: an error frame, then a closed connection
             self.error = e
+            msg = _HDR.pack(_ERR) + f"{type(e).__name__}: {e}".encode()
+            for c in conns:
+                if c is not None:
+                    try:
+                        _send(c, msg)
+                    except OSError:
+                        pass
         finally:
             for c in conns:
                 if c is not None:
@@ -110,8 +125,9 @@ class Rendezvous:
     """Client side: one per rank."""
 
     def __init__(self, rank: int, world: int, address: str, server: RendezvousServer = None,
-                 timeout: float = 600.0):
+                 timeout: float = -1.0):
         self.rank, self.world = rank, world
+        timeout = default_timeout() if timeout is not None and timeout < 0 else timeout
         self.server = server
         host, port = address.rsplit(":", 1)
         deadline = time.time() + 60.0
@@ -126,9 +142,16 @@ class Rendezvous:
         _send(self.sock, str(rank).encode())
 
     def allgather(self, data: bytes) -> list:
-        _send(self.sock, bytes(data))
-        msg = _recv(self.sock)
+        try:
+            _send(self.sock, bytes(data))
+            msg = _recv(self.sock)
+        except (ConnectionError, OSError) as e:
+            err = getattr(self.server, "error", None)
+            raise ConnectionError(f"rendezvous round failed on rank {self.rank}: {e}"
+                                  + (f" (server: {err!r})" if err is not None else "")) from e
         (n,) = _HDR.unpack_from(msg, 0)
+        if n == _ERR:
+            raise ConnectionError(f"rendezvous server failed: {msg[_HDR.size:].decode(errors='replace')}")
         out, off = [], _HDR.size
         for _ in range(n):
             (k,) = _HDR.unpack_from(msg, off)

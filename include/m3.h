@@ -41,6 +41,7 @@ extern "C" {
 #define M3_ERR_RCCL (-4)        /* RCCL error */
 #define M3_ERR_NO_DEVICE (-5)   /* no usable GPU */
 #define M3_ERR_STATE (-6)       /* call out of order (e.g. step before reset) */
+#define M3_ERR_CAP (-7)         /* a safety cap stopped a reset the reference would keep running (see flags) */
 
 /* Per-board flags (uint32 out_flags). */
 #define M3_FLAG_TERMINAL 0x01u    /* n_actions < 1: board returned unchanged (boardv2.py:44-45) */
@@ -82,6 +83,11 @@ int m3_dev_copy(m3_ctx *ctx, void *dst, const void *src, int64_t bytes, int kind
  * (samplerTasks.py:11-13), -1 if the board has no legal action. Nullable outs. */
 int m3_init_boards(m3_ctx *ctx, int64_t n, const uint32_t *seeds, int8_t *out_boards,
                    uint32_t *out_draws, int32_t *out_first_action);
+/* The same, with out_flags[i] (nullable): M3_FLAG_RESET_CAP when reset i stopped after 16384 redraw
+ * rounds (large types = 2 boards; the reference keeps drawing), M3_FLAG_NO_LEGAL when it has no legal
+ * action. m3_init_boards itself returns M3_ERR_CAP (outputs written) if any reset hit the cap. */
+int m3_init_boards_ex(m3_ctx *ctx, int64_t n, const uint32_t *seeds, int8_t *out_boards,
+                      uint32_t *out_draws, int32_t *out_first_action, uint32_t *out_flags);
 
 /* BoardV2.apply_action (boardv2.py:43-207) for n independent (board, seed,
  * n_actions, action) tuples. out_next_action = choice(legal_actions(next))

@@ -47,6 +47,20 @@ def test_bench_spawns_its_ranks_without_a_launcher():
     assert not any(x["torch_loaded"] for x in lines)  # the measurement path never imports torch
 
 
+def test_bench_gather_modes_two_ranks():
+    """--gather final (the N > 1 headline: one all-gather after the last timed step) and --gather step
+    (one per step), both inside the timed region: what each rank's timed loop enqueues, counted on a stub env."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    for mode, want in (("final", 1), ("step", 3 + 1)):
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+               "--gather", mode, "--dry-rendezvous"]
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+        assert out.returncode == 0, out.stderr[-3000:]
+        lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+        assert sorted(x["rank"] for x in lines) == [0, 1]
+        assert all(x["gather"] == mode and x["stub_steps"] == 4 and x["stub_gathers"] == want for x in lines)
+
+
 def test_bench_refuses_a_world_that_differs_from_gpus():
     env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-rendezvous"],
@@ -103,3 +117,21 @@ def test_host_cores_reports_a_usable_count():
     cores, nproc, quota = bench.host_cores()
     assert 1 <= cores <= nproc
     assert quota is None or cores <= quota
+
+
+def test_rendezvous_server_error_reaches_the_clients():
+    """A server that fails (here: two clients claim rank 0) tells the connected clients why, instead of
+    leaving them with a bare closed connection."""
+    import pytest
+
+    sys.path.insert(0, os.path.join(ROOT, "element-crush-gym_amd"))
+    from match3tile.rendezvous import Rendezvous, RendezvousServer
+
+    srv = RendezvousServer(2, timeout=20)
+    a = Rendezvous(0, 2, srv.address, timeout=20)
+    b = Rendezvous(0, 2, srv.address, timeout=20)  # duplicate rank: the server stops
+    with pytest.raises(ConnectionError, match="duplicate rank 0"):
+        a.allgather(b"x")
+    for c in (a, b):
+        c.close()
+    srv.close()

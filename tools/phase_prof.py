@@ -28,7 +28,8 @@ import numpy as np  # noqa: E402
 from match3tile import _native  # noqa: E402
 from match3tile.batched import BatchedMatch3Env  # noqa: E402
 
-PHASES = ["load", "swap", "match", "clear", "drop", "refill", "legal", "next", "reset", "queue", "store"]
+PHASES = ["load", "swap", "match", "clear", "drop", "refill", "legal", "next", "reset", "queue", "store",
+          "tbytes", "tload", "tatom"]
 
 
 def main():
