@@ -452,7 +452,12 @@ int m3_apply_actions(m3_ctx* c, int64_t n, const int8_t* boards, const uint32_t*
         a.ovf_list = (uint32_t*)c->dbuf;
         a.clear_ovf = 1;
         rc = with_shape(c->shape, [&](auto cf) { return launch_apply<decltype(cf)>(c, a); });
-        if (rc) return rc;
+        if (rc) {  // k_apply may have counted overflows that k_apply_fix never cleared: the next
+                   // call must not read them (best effort; the launch error is what is reported)
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipMemset(a.ovf_count, 0, 4);
+            return rc;
+        }
         HIP_TRY(hipStreamSynchronize(c->stream));
         if (*(volatile uint32_t*)(h + im.off[o_bad])) return bad_cells_error();
         memcpy(out_boards, h + im.off[o_b], bytes);
@@ -704,6 +709,7 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         alloc(&e->m397, (size_t)NSLOT * n * 4ull);
         constexpr size_t RW = 1 + EnvCont<decltype(cf)>::WORDS;
         if constexpr (K::CASCADE_LIMIT >= 0) alloc(&e->cont, RW * n * 4ull);
+        if constexpr (RESET_TWO_STAGE<decltype(cf)>) alloc(&e->tab, (size_t)TwoStage<decltype(cf)>::TW * n * 4ull);
         return 0;
     });
     for (hipEvent_t& ev : e->gev)
@@ -781,7 +787,7 @@ int m3_env_destroy(m3_env* e) {
                     e->next_action, e->reward, e->done, e->trunc, e->actions[0], e->actions[1], e->counters,
                     e->ovf_list,
                     e->packed, e->gathered, e->slot, e->ne_words, e->ne_first, e->ne_legal, e->ne_flags,
-                    e->spill, e->m397, e->cont, e->defer};
+                    e->spill, e->m397, e->cont, e->defer, e->tab};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < PF_LAG; ++q)

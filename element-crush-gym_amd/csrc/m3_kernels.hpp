@@ -317,21 +317,6 @@ __device__ __forceinline__ void lds_sync() {
 #endif
 }
 
-// A step's counter block (8 words, EnvArgs::counters) is zeroed by the LAST kernel that reads it,
-// in place of a fill dispatch per shard-step: every block of that launch reads what it needs at
-// its start and takes a ticket (word 7) at its end; the block that draws the last ticket zeroes the
-// block, ticket included, for the step that reuses it PF_LAG steps later.
-__device__ __forceinline__ void zero_block_last(uint32_t* blk) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&blk[7], 1u) == gridDim.x - 1u) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) blk[i] = 0u;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // LDS staging
 // ---------------------------------------------------------------------------
@@ -591,6 +576,11 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
 
 constexpr int NSLOT = 4;            // episode slots per board (see EnvArgs)
 constexpr int PF_LAG = NSLOT - 1;   // steps between a prefetch and its first use
+// Per-shard counter blocks (8 words each), by step % CBLOCKS. Step t's block is read last by its
+// prefetch chain, which step t + PF_LAG waits for; so when step t + PF_LAG's k_env_fix runs, the
+// block of step t + PF_LAG + 1 (= step t's) is free and that kernel zeroes it -- no fill dispatch
+// per shard-step and no cross-block ticket.
+constexpr int CBLOCKS = PF_LAG + 1;
 
 // A reset launch processes "items". Item i is (board b, seed, slot): with a
 // list (env prefetch) b = list[i], seed = list_seed[i], slot = list_slot[i];
@@ -629,7 +619,7 @@ struct InitArgs {
     int64_t cstride;
     uint32_t* defer;             // nullable: items k_init leaves to k_init_coop (reset needs >= RESET_KCAP draws)
     uint32_t* defer_count;       // device count for defer (zeroed before k_init)
-    uint32_t* zero_at_end;       // nullable: the step's counter block; the chain's last kernel zeroes it
+    uint32_t* tab;               // nullable: two-stage reset table rows [n][TwoStage::TW] (16x16x8 prefetch)
 };
 }  // namespace m3k
 using m3k::InitArgs;
@@ -922,7 +912,6 @@ __global__ void __launch_bounds__(64) k_init_coop(InitArgs a) {
         wave_reset<CF>(a, a.defer[q], key_s, cell_s, lane);
         if (a.stats && lane == 0) atomicAdd(&a.stats[1], 1u);
     }
-    if (a.zero_at_end) zero_block_last(a.zero_at_end);  // the env prefetch chain ends here (9x9)
 }
 
 // ---- lane-per-board reset for boards that need >= 624 draws -------------
@@ -1027,7 +1016,6 @@ __global__ void __launch_bounds__(INIT_FIX_BLOCK) k_init_fix_lane(InitArgs a) {
         const uint64_t m = __ballot(long_reset);
         if (m && a.stats && (threadIdx.x & 63) == 0) atomicAdd(&a.stats[1], (uint32_t)__popcll(m));
     }
-    if (a.zero_at_end) zero_block_last(a.zero_at_end);  // the env prefetch chain ends here (16x16, frames)
 }
 
 // One round of randint(1, T+1, (R, C)) for a power-of-two T (every draw is a
@@ -1117,6 +1105,269 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init_chain2(InitArgs a) {
     }
 }
 
+// ---- two-stage reset (16x16x8 env prefetch) -----------------------------
+// Each round of BoardV2.__init__'s redraw loop draws a whole (R, C) board
+// (boardv2.py:21, :25), and with a power-of-two tile count every draw is a
+// tile, so round k of a reset is raw outputs [k*N, (k+1)*N) of its seed's
+// MT19937 stream, whatever the match masks turn out to be. The reset splits:
+//   k_reset_stream: G resets per wave. Each lane runs init_genrand of one
+//     board into LDS (VALU: the recurrence is serial per board), then the wave
+//     twists each board's 624-word state and packs its first ROUNDS rounds of
+//     tiles as raw-bit planes (one ballot per bit per 64 draws) into a table
+//     row of TW words, written with one coalesced store;
+//   k_reset_tiles: one board per lane, the match-mask loop of boardv2.py:23-27
+//     over the table rounds (16-B loads), then the outputs of init_outputs.
+// A reset that needs a round past ROUNDS (~2 %) goes to k_init_coop's defer
+// list (one wave per board, from the seed). This replaces the lane-private
+// 2.5 KB FullMT state that k_init_fix_lane walks in scratch.
+#ifndef M3_RESET16_TWO_STAGE
+#define M3_RESET16_TWO_STAGE 1
+#endif
+#ifndef M3_TS_BOARDS
+#define M3_TS_BOARDS 4
+#endif
+#ifndef M3_TS_INTERLEAVE
+#define M3_TS_INTERLEAVE 4
+#endif
+template <class CF, bool DYN = CF::DYN>  // (frame configurations have no compile-time tile range)
+struct TwoStageOk : std::false_type {};
+template <class CF>
+struct TwoStageOk<CF, false>
+    : std::bool_constant<M3_RESET16_TWO_STAGE && (CF::N > 128) && CF::N % 64 == 0 && CF::TILE_RNG != 0u &&
+                         CF::TILE_RNG == CF::TILE_MASK> {};
+template <class CF>
+constexpr bool RESET_TWO_STAGE = TwoStageOk<CF>::value;
+template <class CF>
+struct TwoStage {
+    static constexpr int RB = __builtin_popcount(CF::TILE_MASK);  // raw bits per tile
+    static constexpr int ROUNDS = 4;
+    static constexpr int DRAWS = ROUNDS * CF::N;                  // 16x16x8: 1024
+    static_assert(DRAWS > 624 && DRAWS - 624 <= 624, "the first block and part of the second");
+    static constexpr int GROUPS = DRAWS / 64;
+    static constexpr int RW = CF::W * RB;                         // table words per round
+    static constexpr int TW = (ROUNDS * RW + 1 + 3) / 4 * 4;      // + mt[397], rows 16-B aligned
+    static_assert(ROUNDS * RW <= 128 && RW % 4 == 0, "row = two lane words; rounds on 16 B");
+    static constexpr int G = M3_TS_BOARDS;                        // boards per wave
+    static constexpr int U = M3_TS_INTERLEAVE;                    // boards twisted / packed together
+    static_assert(G % U == 0, "whole interleave groups");
+    static_assert(G >= 1 && G <= 64, "one lane per board in the init");
+    static constexpr int KST = 625;  // LDS words per board: odd, so the init's lanes hit distinct banks
+};
+
+// The MT19937 twist of U boards' states at once (key + u * stride; the first nu
+// are real), so each trip's LDS latency is paid once for U boards.
+template <int U>
+__device__ __forceinline__ void wave_twist_u(uint32_t* key, int stride, int nu, int lane) {
+    for (int base = 0; base < 227; base += 64) {  // mt'[i] = mt[i+397] ^ twist(mt[i], mt[i+1])
+        const int i = base + lane;
+        uint32_t a0[U], a1[U], x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t* k = key + u * stride;
+            a0[u] = a1[u] = x[u] = 0u;
+            if (u < nu && i < 227) { a0[u] = k[i]; a1[u] = k[i + 1]; x[u] = k[i + 397]; }
+        }
+        asm volatile("" ::: "memory");  // every lane's loads before any lane's store
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u < nu && i < 227) key[u * stride + i] = x[u] ^ mt_twist(a0[u], a1[u]);
+        wave_sync();
+    }
+    for (int base = 227; base < 623; base += 64) {  // mt'[i] = mt'[i-227] ^ twist(mt[i], mt[i+1])
+        const int i = base + lane;
+        uint32_t a0[U], a1[U], x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t* k = key + u * stride;
+            a0[u] = a1[u] = x[u] = 0u;
+            if (u < nu && i < 623) { a0[u] = k[i]; a1[u] = k[i + 1]; x[u] = k[i - 227]; }
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u < nu && i < 623) key[u * stride + i] = x[u] ^ mt_twist(a0[u], a1[u]);
+        wave_sync();
+    }
+    if (lane < nu) {
+        uint32_t* k = key + lane * stride;
+        k[623] = k[396] ^ mt_twist(k[623], k[0]);
+    }
+    wave_sync();
+}
+
+// The first NW words of the next MT block of U boards, out of place (nxt + u * NW;
+// key keeps the current block): nxt[i] = (i < 227 ? key[i + 397] : nxt[i - 227]) ^
+// twist(key[i], key[i + 1]). Draws past the table's last round are never made.
+template <int U, int NW>
+__device__ __forceinline__ void wave_twist_next_u(const uint32_t* key, int stride, uint32_t* nxt, int nu, int lane) {
+    static_assert(NW > 227 && NW <= 623, "both twist phases, no wrap word");
+    for (int base = 0; base < NW; base += 64) {  // phase 2 reads nxt[i - 227] of an earlier trip
+        const int i = base + lane;
+        uint32_t a0[U], a1[U], x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t* k = key + u * stride;
+            a0[u] = a1[u] = x[u] = 0u;
+            if (u < nu && i < NW) {
+                a0[u] = k[i];
+                a1[u] = k[i + 1];
+                x[u] = i < 227 ? k[i + 397] : nxt[u * NW + i - 227];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u < nu && i < NW) nxt[u * NW + i] = x[u] ^ mt_twist(a0[u], a1[u]);
+        wave_sync();
+    }
+}
+
+template <class CF>
+__global__ void __launch_bounds__(64) k_reset_stream(InitArgs a) {
+    using TS = TwoStage<CF>;
+    constexpr int NX = TS::DRAWS - 624;  // words of the second block
+    constexpr int U = TS::U;
+    __shared__ uint32_t key_s[TS::G * TS::KST + U * NX];
+    uint32_t* nxt = key_s + TS::G * TS::KST;
+    const int lane = (int)threadIdx.x;
+    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
+    for (int64_t base = (int64_t)blockIdx.x * TS::G; base < cnt; base += (int64_t)gridDim.x * TS::G) {
+        const int nb = (int)(cnt - base < TS::G ? cnt - base : TS::G);
+        if (lane < nb) {  // init_genrand(seed), one board per lane
+            int64_t b;
+            uint32_t seed, slot;
+            init_item(a, base + lane, b, seed, slot);
+            uint32_t* k = key_s + lane * TS::KST;
+            uint32_t x = seed;
+            k[0] = x;
+#pragma unroll 8
+            for (uint32_t i = 1; i < 624u; ++i) {
+                x = mt_init_next(x, i);
+                k[i] = x;
+            }
+        }
+        wave_sync();
+#pragma unroll 1
+        for (int j0 = 0; j0 < nb; j0 += U) {
+            const int nu = nb - j0 < U ? nb - j0 : U;
+            uint32_t* key = key_s + j0 * TS::KST;
+            const uint32_t m397 = lane < nu ? key[lane * TS::KST + 397] : 0u;  // lane u: board j0 + u
+            wave_sync();
+            wave_twist_u<U>(key, TS::KST, nu, lane);                  // draws 0 .. 623
+            wave_twist_next_u<U, NX>(key, TS::KST, nxt, nu, lane);    // draws 624 .. DRAWS - 1
+            uint32_t o0[U], o1[U];                                    // row words lane and 64 + lane
+#pragma unroll
+            for (int u = 0; u < U; ++u) o0[u] = o1[u] = 0u;
+#pragma unroll 1
+            for (int g = 0; g < TS::GROUPS; ++g) {
+                const int d = g * 64 + lane;
+                uint32_t y[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)  // randint(1, T+1) - 1: every draw a tile
+                    y[u] = mt_temper(d < 624 ? key[u * TS::KST + d] : nxt[u * NX + d - 624]) & CF::TILE_MASK;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+#pragma unroll
+                    for (int q = 0; q < TS::RB; ++q) {
+                        const uint64_t bal = __ballot((y[u] >> q) & 1u);
+                        const int idx = (g * TS::RB + q) * 2;  // words idx (draws 0-31) and idx + 1 (32-63)
+                        const uint32_t val = (lane & 1) ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+                        if ((lane & ~1) == (idx & 63)) {
+                            if (idx < 64) o0[u] = val;
+                            else o1[u] = val;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (u < nu) {
+                    uint32_t* row = a.tab + (base + j0 + u) * TS::TW;
+                    row[lane] = o0[u];
+                    if (lane < TS::ROUNDS * TS::RW - 64) row[64 + lane] = o1[u];
+                }
+            }
+            if (lane < nu) a.tab[(base + j0 + lane) * TS::TW + TS::ROUNDS * TS::RW] = m397;
+            wave_sync();
+        }
+    }
+}
+
+// round k of the table row into the planes: value = raw + 1, under `only`
+template <class CF>
+__device__ __forceinline__ void tab_round(typename CF::Bd* P, const uint32_t* t, const typename CF::Bd* only) {
+    using TS = TwoStage<CF>;
+    uint32_t raw[TS::RW];
+#pragma unroll
+    for (int q = 0; q < TS::RW; q += 4) {
+        const uint4 x = *reinterpret_cast<const uint4*>(t + q);
+        raw[q] = x.x;
+        raw[q + 1] = x.y;
+        raw[q + 2] = x.z;
+        raw[q + 3] = x.w;
+    }
+#pragma unroll
+    for (int w = 0; w < CF::W; ++w) {
+        uint32_t c = 0xFFFFFFFFu;  // + 1: a ripple carry over the bit planes
+        const uint32_t m = only ? only->w[w] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int p = 0; p < CF::BITS; ++p) {
+            const uint32_t r = p < TS::RB ? raw[((w >> 1) * TS::RB + (p < TS::RB ? p : 0)) * 2 + (w & 1)] : 0u;
+            const uint32_t vb = r ^ c;
+            c &= r;
+            P[p].w[w] = (P[p].w[w] & ~m) | (vb & m);
+        }
+    }
+}
+
+template <class CF>
+__global__ void __launch_bounds__(64) k_reset_tiles(InitArgs a) {
+    using TS = TwoStage<CF>;
+    const typename CF::Dim dm{};
+    const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
+    if (a.stats && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], (uint32_t)cnt);
+    for (int64_t base = (int64_t)blockIdx.x * 64; base < cnt; base += (int64_t)gridDim.x * 64) {
+        const int64_t i = base + threadIdx.x;
+        bool ok = true, long_reset = false;
+        if (i < cnt) {
+            int64_t b;
+            uint32_t seed, slot;
+            init_item(a, i, b, seed, slot);
+            const uint32_t* t = a.tab + i * TS::TW;
+            const uint32_t m397 = t[TS::ROUNDS * TS::RW];
+            typename CF::Bd P[CF::NP], mask;
+#pragma unroll
+            for (int p = 0; p < CF::NP; ++p) P[p] = CF::Bd::zero();
+            tab_round<CF>(P, t, nullptr);                                  // boardv2.py:21
+            uint32_t rounds = 0;
+            while (get_match_mask<CF>(P, mask)) {                          // :23-27
+                if (++rounds >= (uint32_t)TS::ROUNDS) {
+                    ok = false;
+                    break;
+                }
+                tab_round<CF>(P, t + rounds * TS::RW, &mask);
+            }
+            if (ok) {
+                if (a.m397) a.m397[(int64_t)slot * a.cstride + b] = m397;
+                const int64_t ob = (int64_t)slot * a.sstride + b;
+                const uint32_t draws = (rounds + 1u) * (uint32_t)CF::N;
+                init_outputs<CF>(a, b, ob, seed, m397, draws, P, dm);
+                init_store_board<CF>(a, ob, P, dm);
+                long_reset = draws >= 624u;
+            }
+        }
+        const uint64_t bad = __ballot(!ok);
+        const int lane = (int)threadIdx.x;
+        if (bad) {  // left to k_init_coop (one wave per board): one wave-aggregated append
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(a.defer_count, (uint32_t)__popcll(bad));
+            q = __shfl(q, 0);
+            if (!ok) a.defer[q + (uint32_t)__popcll(bad & ((1ull << lane) - 1ull))] = (uint32_t)i;
+        }
+        const uint64_t lm = __ballot(long_reset);
+        if (lm && a.stats && lane == 0) atomicAdd(&a.stats[1], (uint32_t)__popcll(lm));
+    }
+}
+
 // mt[397] of init_genrand(seeds[b]): the chain word of each board's current
 // episode (env resume, m3_env_set)
 __global__ void __launch_bounds__(256) k_mt397(int64_t n, const uint32_t* seeds, uint32_t* out) {
@@ -1195,7 +1446,7 @@ struct EnvArgs {
     int64_t cstride;
     uint32_t* cont;        // nullable: continuation records of paused steps (k_env_cont_grid), [1 + WORDS][cont_stride]
     int64_t cont_stride;
-    int zero_at_fix;       // k_env_fix zeroes the counter block (no prefetch chain reads it after the step)
+    uint32_t* zero_next;   // the counter block of the next step, zeroed by k_env_fix (see CBLOCKS)
 };
 }  // namespace m3k
 using m3k::EnvArgs;
@@ -1498,6 +1749,7 @@ template <class CF>
 __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
     const uint32_t cnt = a.counters[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], cnt);
+    if (a.zero_next && blockIdx.x == 0 && threadIdx.x < 8) a.zero_next[threadIdx.x] = 0u;  // (CBLOCKS)
     const typename CF::Dim dm(a.shape);
     for (uint32_t i = blockIdx.x * lanes_for<CF>() + threadIdx.x; threadIdx.x < lanes_for<CF>() && i < cnt;
          i += gridDim.x * lanes_for<CF>()) {
@@ -1525,7 +1777,6 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
         }
         planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
     }
-    if (a.zero_at_fix) zero_block_last(a.counters);
 }
 
 // ---------------------------------------------------------------------------
@@ -1739,7 +1990,7 @@ struct m3_env {
     bool upload_this = false;              // the step being enqueued reads actions[step & 1]
     // counters, 64 words per shard: [8q + 0] step overflow count, [8q + 1]
     // prefetch queue length, [8q + 2] deferred prefetch resets, [8q + 3] spill
-    // records taken, [8q + 4] continuation records (q = step % PF_LAG); stats
+    // records taken, [8q + 4] continuation records (q = step % CBLOCKS); stats
     // [40] step recomputes, [41] resets, [42] reset recomputes; [48 + k] the
     // reset / slot-fill overflow counts (shard 0's block)
     uint32_t* counters = nullptr;
@@ -1755,6 +2006,7 @@ struct m3_env {
     uint32_t* m397 = nullptr;  // [NSLOT][n]
     uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont_grid)
     uint32_t* defer = nullptr; // prefetch resets k_init leaves to k_init_coop [n]
+    uint32_t* tab = nullptr;   // two-stage reset table rows [n][TwoStage::TW] (16x16x8)
     // prefetch queues and their overflow lists, by step % PF_LAG
     uint32_t *pf_list[PF_LAG] = {}, *pf_seed[PF_LAG] = {}, *pf_slot[PF_LAG] = {};
     int64_t steps = 0;
@@ -1838,6 +2090,19 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
             gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
             hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
         }
+    } else if (RESET_TWO_STAGE<CF> && a.tab && a.defer) {  // 16x16x8 env prefetch (see k_reset_stream)
+        if constexpr (RESET_TWO_STAGE<CF>) {
+            const InitArgs& s = a;
+            int64_t ga = (max_items + TwoStage<CF>::G - 1) / TwoStage<CF>::G;
+            ga = ga > 2048 ? 2048 : ga;
+            hipLaunchKernelGGL(k_reset_stream<CF>, dim3((unsigned)ga), dim3(64), 0, stream, s);
+            HIP_TRY(hipGetLastError());
+            hipLaunchKernelGGL(k_reset_tiles<CF>, dim3((unsigned)(g > 4096 ? 4096 : g)), dim3(64), 0, stream, s);
+            HIP_TRY(hipGetLastError());
+            int64_t gc = max_items / 32 + 1;  // the ~2 % past the table's rounds
+            gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+            hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
+        }
     } else {  // frame shapes: FullMT (lane-private scratch); 32 x 32 frame: one board per wave
         const int64_t gl = (max_items + lanes_for<CF>() - 1) / lanes_for<CF>();
         hipLaunchKernelGGL(k_init_fix_lane<CF>, dim3((unsigned)(gl > 4096 ? 4096 : gl)), dim3(INIT_FIX_BLOCK), 0,
@@ -1866,6 +2131,7 @@ void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
     r.m397 = e->m397 + o;
     r.slot_flags = e->ne_flags + o;
     r.cstride = e->n;
+    if constexpr (RESET_TWO_STAGE<CF>) r.tab = e->tab ? e->tab + o * TwoStage<CF>::TW : nullptr;
 }
 
 // Enqueue one env step of shard s: on the step stream, wait for the prefetch
@@ -1884,7 +2150,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     const int N = c->N, AW = c->AW;
     const int par = (int)(e->steps % PF_LAG);
     uint32_t* base = e->counters + 64 * s;
-    uint32_t* cnt = base + 8 * par;
+    uint32_t* cnt = base + 8 * (e->steps % CBLOCKS);
     hipStream_t st = sh.stream;
     const int pb = (int)(e->steps & 1);  // packed buffer of this step
     if (e->upload_this) HIP_TRY(hipStreamWaitEvent(st, e->upload_ev[pb], 0));  // host actions in actions[pb]
@@ -1929,7 +2195,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.cstride = e->n;
     a.cont = KS<CF>::CASCADE_LIMIT >= 0 ? e->cont + o : nullptr;
     a.cont_stride = e->n;
-    a.zero_at_fix = !e->autoreset;  // (with autoreset the prefetch chain is the block's last reader)
+    a.zero_next = base + 8 * ((e->steps + 1) % CBLOCKS);
     const bool timed = e->tn < e->tcap;
     if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], st));
     hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
@@ -1960,8 +2226,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.list_slot = e->pf_slot[par] + o;
         r.list_count = &cnt[1];
         r.stats = base + 41;
-        r.zero_at_end = cnt;  // the chain's last kernel zeroes this step's counter block
-        if constexpr (INIT_INLINE_FIX<CF> || (!CF::DYN && M3_RESET16_CHAIN2)) {
+        if constexpr (INIT_INLINE_FIX<CF> || (!CF::DYN && M3_RESET16_CHAIN2) || RESET_TWO_STAGE<CF>) {
             r.defer = e->defer + o;
             r.defer_count = &cnt[2];  // zeroed with the block
         }

@@ -170,9 +170,11 @@ def test_frame_env_large_batch_vs_oracle(shape):
                          ids=lambda s: "x".join(map(str, s)))
 def test_frame_rollouts_vs_oracle(shape):
     """MCTS rollouts (f3) of 4096 states, 64 lanes a wave, on frame shapes of every token width.
-    (Regression: with ~1,500 SGPR spills in k_rollout some of these shapes came out wrong for a
-    lane only when other lanes of its wave were active -- the frame action-id packing now runs as
-    a rolled loop, tools/dbg.)"""
+    Regression guard for the round-4 lane interference: a value live out of a
+    divergent loop (the RNG position after the cascade) came back as garbage for lanes that had
+    left the loop early, in kernels that spilled VGPRs -- a board was exact alone and wrong only
+    with busy neighbours. Fails on the pre-fix library (build/libm3_pre.so: 55 / 70 / 1,662 of
+    4,096 wrong on 12x12x7 / 10x8x5 / 10x8x9, profiles/r05_lane_regression.txt), passes now."""
     R, C, T = shape
     ctx = _native.Context(R, C, T)
     seeds = np.arange(1, 4097, dtype=np.uint32)
