@@ -1155,68 +1155,49 @@ struct TwoStage {
 };
 
 // The MT19937 twist of U boards' states at once (key + u * stride; the first nu
-// are real), so each trip's LDS latency is paid once for U boards.
-template <int U>
+// are real), in place, so each trip's LDS latency is paid once for U boards.
+// NW = 624: the whole block; NW < 624: only words [0, NW) of the next block
+// (the draws past the table's last round are never made) -- words [NW, 624)
+// keep the current block's values.
+template <int U, int NW = 624>
 __device__ __forceinline__ void wave_twist_u(uint32_t* key, int stride, int nu, int lane) {
-    for (int base = 0; base < 227; base += 64) {  // mt'[i] = mt[i+397] ^ twist(mt[i], mt[i+1])
+    static_assert(NW == 624 || (NW > 227 && NW <= 576), "a whole block, or a head of the next");
+    constexpr int E1 = NW < 227 ? NW : 227, E2 = NW == 624 ? 623 : NW;
+    for (int base = 0; base < E1; base += 64) {  // mt'[i] = mt[i+397] ^ twist(mt[i], mt[i+1])
         const int i = base + lane;
         uint32_t a0[U], a1[U], x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t* k = key + u * stride;
             a0[u] = a1[u] = x[u] = 0u;
-            if (u < nu && i < 227) { a0[u] = k[i]; a1[u] = k[i + 1]; x[u] = k[i + 397]; }
+            if (u < nu && i < E1) { a0[u] = k[i]; a1[u] = k[i + 1]; x[u] = k[i + 397]; }
         }
         asm volatile("" ::: "memory");  // every lane's loads before any lane's store
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (u < nu && i < 227) key[u * stride + i] = x[u] ^ mt_twist(a0[u], a1[u]);
+            if (u < nu && i < E1) key[u * stride + i] = x[u] ^ mt_twist(a0[u], a1[u]);
         wave_sync();
     }
-    for (int base = 227; base < 623; base += 64) {  // mt'[i] = mt'[i-227] ^ twist(mt[i], mt[i+1])
+    for (int base = 227; base < E2; base += 64) {  // mt'[i] = mt'[i-227] ^ twist(mt[i], mt[i+1])
         const int i = base + lane;
         uint32_t a0[U], a1[U], x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t* k = key + u * stride;
             a0[u] = a1[u] = x[u] = 0u;
-            if (u < nu && i < 623) { a0[u] = k[i]; a1[u] = k[i + 1]; x[u] = k[i - 227]; }
+            if (u < nu && i < E2) { a0[u] = k[i]; a1[u] = k[i + 1]; x[u] = k[i - 227]; }
         }
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (u < nu && i < 623) key[u * stride + i] = x[u] ^ mt_twist(a0[u], a1[u]);
+            if (u < nu && i < E2) key[u * stride + i] = x[u] ^ mt_twist(a0[u], a1[u]);
         wave_sync();
     }
-    if (lane < nu) {
-        uint32_t* k = key + lane * stride;
-        k[623] = k[396] ^ mt_twist(k[623], k[0]);
-    }
-    wave_sync();
-}
-
-// The first NW words of the next MT block of U boards, out of place (nxt + u * NW;
-// key keeps the current block): nxt[i] = (i < 227 ? key[i + 397] : nxt[i - 227]) ^
-// twist(key[i], key[i + 1]). Draws past the table's last round are never made.
-template <int U, int NW>
-__device__ __forceinline__ void wave_twist_next_u(const uint32_t* key, int stride, uint32_t* nxt, int nu, int lane) {
-    static_assert(NW > 227 && NW <= 623, "both twist phases, no wrap word");
-    for (int base = 0; base < NW; base += 64) {  // phase 2 reads nxt[i - 227] of an earlier trip
-        const int i = base + lane;
-        uint32_t a0[U], a1[U], x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t* k = key + u * stride;
-            a0[u] = a1[u] = x[u] = 0u;
-            if (u < nu && i < NW) {
-                a0[u] = k[i];
-                a1[u] = k[i + 1];
-                x[u] = i < 227 ? k[i + 397] : nxt[u * NW + i - 227];
-            }
+    if constexpr (NW == 624) {
+        if (lane < nu) {
+            uint32_t* k = key + lane * stride;
+            k[623] = k[396] ^ mt_twist(k[623], k[0]);
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (u < nu && i < NW) nxt[u * NW + i] = x[u] ^ mt_twist(a0[u], a1[u]);
         wave_sync();
     }
 }
@@ -1225,9 +1206,10 @@ template <class CF>
 __global__ void __launch_bounds__(64) k_reset_stream(InitArgs a) {
     using TS = TwoStage<CF>;
     constexpr int NX = TS::DRAWS - 624;  // words of the second block
+    constexpr int G1 = 624 / 64;         // 64-draw groups wholly in the first block
+    static_assert(NX <= G1 * 64, "the second twist must leave the straddling group's first-block words");
     constexpr int U = TS::U;
-    __shared__ uint32_t key_s[TS::G * TS::KST + U * NX];
-    uint32_t* nxt = key_s + TS::G * TS::KST;
+    __shared__ uint32_t key_s[TS::G * TS::KST];
     const int lane = (int)threadIdx.x;
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
     for (int64_t base = (int64_t)blockIdx.x * TS::G; base < cnt; base += (int64_t)gridDim.x * TS::G) {
@@ -1252,18 +1234,16 @@ __global__ void __launch_bounds__(64) k_reset_stream(InitArgs a) {
             uint32_t* key = key_s + j0 * TS::KST;
             const uint32_t m397 = lane < nu ? key[lane * TS::KST + 397] : 0u;  // lane u: board j0 + u
             wave_sync();
-            wave_twist_u<U>(key, TS::KST, nu, lane);                  // draws 0 .. 623
-            wave_twist_next_u<U, NX>(key, TS::KST, nxt, nu, lane);    // draws 624 .. DRAWS - 1
-            uint32_t o0[U], o1[U];                                    // row words lane and 64 + lane
+            uint32_t o0[U], o1[U];  // row words lane and 64 + lane
 #pragma unroll
             for (int u = 0; u < U; ++u) o0[u] = o1[u] = 0u;
-#pragma unroll 1
-            for (int g = 0; g < TS::GROUPS; ++g) {
+            // draws 64g .. 64g + 63 into the row: one ballot per raw bit and board
+            auto pack = [&](int g) {
                 const int d = g * 64 + lane;
+                const int w = d < 624 ? d : d - 624;  // (the straddling group: first-block words >= NX)
                 uint32_t y[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u)  // randint(1, T+1) - 1: every draw a tile
-                    y[u] = mt_temper(d < 624 ? key[u * TS::KST + d] : nxt[u * NX + d - 624]) & CF::TILE_MASK;
+                for (int u = 0; u < U; ++u) y[u] = mt_temper(key[u * TS::KST + w]) & CF::TILE_MASK;  // randint - 1
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -1277,7 +1257,14 @@ __global__ void __launch_bounds__(64) k_reset_stream(InitArgs a) {
                         }
                     }
                 }
-            }
+            };
+            wave_twist_u<U>(key, TS::KST, nu, lane);  // draws 0 .. 623
+#pragma unroll 1
+            for (int g = 0; g < G1; ++g) pack(g);
+            wave_sync();
+            wave_twist_u<U, NX>(key, TS::KST, nu, lane);  // draws 624 .. DRAWS - 1, over words [0, NX)
+#pragma unroll 1
+            for (int g = G1; g < TS::GROUPS; ++g) pack(g);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (u < nu) {

@@ -166,14 +166,15 @@ def test_frame_env_large_batch_vs_oracle(shape):
     env.close()
 
 
-@pytest.mark.parametrize("shape", [(10, 8, 5), (12, 12, 7), (10, 10, 6), (10, 8, 9), (16, 16, 15)],
+@pytest.mark.parametrize("shape", [(10, 8, 5), (12, 12, 7), (10, 10, 6), (10, 8, 9), (16, 16, 15), (10, 8, 3),
+                                   (12, 12, 20)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_frame_rollouts_vs_oracle(shape):
     """MCTS rollouts (f3) of 4096 states, 64 lanes a wave, on frame shapes of every token width.
     Regression guard for the round-4 lane interference: a value live out of a
     divergent loop (the RNG position after the cascade) came back as garbage for lanes that had
     left the loop early, in kernels that spilled VGPRs -- a board was exact alone and wrong only
-    with busy neighbours. Fails on the pre-fix library (build/libm3_pre.so: 55 / 70 / 1,662 of
+    with busy neighbours. Token widths 2..5 bits. Fails on the pre-fix library (build/libm3_pre.so: 55 / 70 / 1,662 of
     4,096 wrong on 12x12x7 / 10x8x5 / 10x8x9, profiles/r05_lane_regression.txt), passes now."""
     R, C, T = shape
     ctx = _native.Context(R, C, T)

@@ -1,0 +1,58 @@
+"""Register census of the built gfx950 kernels (round 5, DESIGN.md §4 "Lane interference").
+
+The round-4 lane interference needed a kernel that runs several boards per wave AND spills: the
+RNG position carried out of the divergent cascade loop came back stale for the lanes that had left
+the loop early. The frame kernels now run that loop wave-uniform; this census keeps the 16 x 16
+frame's board-per-lane step kernels out of scratch (at most a few values spilled to AGPRs) and holds every kernel to the spill counts
+committed in profiles/r05_spill_audit.json (a ratchet: a build that spills more fails here, on the
+CPU, before any GPU run). Reads the code-object metadata of build/m3_inst_*.o (tools/spill_audit.py).
+"""
+import glob
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import spill_audit  # noqa: E402
+
+OBJS = sorted(glob.glob(os.path.join(ROOT, "element-crush-gym_amd", "build", "m3_inst_*.o")))
+REF = os.path.join(ROOT, "profiles", "r05_spill_audit.json")
+pytestmark = pytest.mark.skipif(len(OBJS) < 10, reason="library objects not built (make -C element-crush-gym_amd)")
+
+# board-per-lane kernels of the 16 x 16 frame that must keep every value in registers (a few spill
+# into AGPRs, no scratch): the env step, the stateless apply / legal kernels, the reset
+IN_REGS = ("k_env_step<", "k_apply<", "k_legal<", "k_init_fix_lane<")
+
+
+@pytest.fixture(scope="module")
+def census():
+    return spill_audit.census(OBJS)
+
+
+def test_census_covers_every_configuration(census):
+    for tag in ("9x9x6", "16x16x8", "frame16/bits2", "frame16/bits5", "frame32/bits2", "frame32/bits5"):
+        assert any(tag in k for k in census), tag
+
+
+def test_frame16_step_kernels_do_not_spill_to_scratch(census):
+    checked = 0
+    for name, v in census.items():
+        if "frame16/" in name and name.startswith(IN_REGS):
+            scratch = v.get("private_segment_fixed_size", 0)
+            if name.startswith("k_init_fix_lane<"):
+                scratch -= 2516  # its FullMT state: a lane-private array by design, not a spill
+            assert scratch == 0 and v.get("vgpr_spill_count", 0) <= 5, (name, v)
+            checked += 1
+    assert checked == 16
+
+
+def test_no_kernel_spills_more_than_committed(census):
+    with open(REF) as f:
+        ref = json.load(f)
+    worse = {k: (v.get("vgpr_spill_count", 0), ref[k].get("vgpr_spill_count", 0))
+             for k, v in census.items()
+             if k in ref and v.get("vgpr_spill_count", 0) > ref[k].get("vgpr_spill_count", 0)}
+    assert not worse, worse

@@ -41,7 +41,7 @@ open(os.path.join(P, f"{tag}_pmc.txt"), "w").write(pmc)
 
 PIPE = ("k_env_step", "k_env_cont", "k_env_cont_grid", "k_env_fix")
 # every kernel that runs inside a timed step: the step pipeline and the autoreset (prefetch) kernels
-STEP_KERNELS = PIPE + ("k_init", "k_init_coop", "k_init_fix_lane", "k_init_chain2")
+STEP_KERNELS = PIPE + ("k_init", "k_init_coop", "k_init_fix_lane", "k_init_chain2", "k_reset_stream", "k_reset_tiles")
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 # the SQ pass, per dispatch: (dispatch id, kernel, SQ_INSTS_VALU summed over its records)
 disp = collections.defaultdict(lambda: [None, 0.0])

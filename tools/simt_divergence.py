@@ -99,7 +99,7 @@ int main(int argc, char** argv) {
   }
   const double waves = (double)nb / 64 * steps, lanes_n = (double)nb * steps;
   printf("cascade iterations: per board %.2f, per wave (max over lanes) %.2f\n", lane_iters / lanes_n, wave_iters / waves);
-  const char* names[] = {"", "match run starts", "special triggers", "gravity passes", "refill draws", "spawn groups", "group search"};
+  const char* names[] = {"", "match run starts", "special triggers", "gravity passes/stages", "refill draws", "spawn groups", "group search"};
   for (auto& kv : wave_trips)
     printf("%-17s per board %6.2f  per wave %6.2f  SIMT efficiency %.2f\n", names[kv.first],
            lane_trips[kv.first] / lanes_n, kv.second / waves, lane_trips[kv.first] / (kv.second * 64));
@@ -114,10 +114,13 @@ PATCHES = [  # (anchor, text inserted after it)
     ("    while (cand.any()) {                                       // row-major scan over run starts", "\n        SIM_TRIP(1);"),
     ("    while (trig.any()) {\n        const int x = trig.lowest();", "\n        SIM_TRIP(2);"),
     ("    for (;;) {  // drop every tile that has a hole somewhere below it by one row", "\n        SIM_TRIP(3);"),
+    # round 5: the decomposed gravity -- a stage counts for a lane that still has holes to close
+    ("        constexpr int D = (1 << decltype(S)::value) * C;  // rows moved in this stage, as bits",
+     "\n        if (mk.any()) SIM_TRIP(3);"),
     ("        uint32_t v = rng.next32() & tmask;", "\n        SIM_TRIP(4);"),
     ("        for (int gi = 0; gi < ng; ++gi) {                      // get_match_spawn_mask (:159-169)", "\n            SIM_TRIP(5);"),
     ("                    if ((st.get_v(gi) & rh).any()) { g = gi; break; }", "\n                    SIM_TRIP(6);"),
-    ("                ++it;",
+    ("                ++it;\n                const Bd em = gravity<CF>(P, dm);               // :166-173",
      "\n                SIM_ITER();\n                SIM_HOLES(VALID.andnot(tb_nonzero<CF>(P) | special_mask<CF, 6>(P)).popc());"),
 ]
 
