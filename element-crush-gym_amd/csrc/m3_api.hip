@@ -951,6 +951,12 @@ int m3_env_get(m3_env* e, int what, void* host_out) {
     if (rc) return rc;
     rc = join_shards(e, e->ctx->stream);
     if (rc) return rc;
+    if (what == M3_ENV_LEGAL && !e->legal_eager) {  // derived on request from the current boards
+        rc = with_shape(e->ctx->shape, [&](auto cf) {
+            return launch_legal<decltype(cf)>(e->ctx, e->n, e->boards[e->cur], e->legal);
+        });
+        if (rc) return rc;
+    }
     HIP_TRY(hipMemcpyAsync(host_out, p, bytes, hipMemcpyDeviceToHost, e->ctx->stream));
     HIP_TRY(hipStreamSynchronize(e->ctx->stream));
     return M3_OK;
@@ -1003,7 +1009,21 @@ int m3_env_comm_size(m3_env* e, int* out) {
 int m3_env_device_ptr(m3_env* e, int what, void** out) {
     CHECK_ARG(e && out, "bad arguments");
     size_t bytes;
-    return env_field(e, what, out, &bytes);
+    int rc = env_field(e, what, out, &bytes);
+    if (rc || what != M3_ENV_LEGAL || e->legal_eager) return rc;
+    // a device consumer of the legal sets: from now on every step writes them; fill the buffer now
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    rc = ensure_fresh(e);
+    if (rc) return rc;
+    rc = join_shards(e, e->ctx->stream);
+    if (rc) return rc;
+    rc = with_shape(e->ctx->shape, [&](auto cf) {
+        return launch_legal<decltype(cf)>(e->ctx, e->n, e->boards[e->cur], e->legal);
+    });
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(e->ctx->stream));
+    e->legal_eager = true;
+    return M3_OK;
 }
 
 int m3_comm_unique_id(uint8_t out_id[128]) {

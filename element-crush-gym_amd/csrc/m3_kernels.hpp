@@ -1126,6 +1126,9 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init_chain2(InitArgs a) {
 #ifndef M3_TS_BOARDS
 #define M3_TS_BOARDS 4
 #endif
+#ifndef M3_TS_ROUNDS  // redraw rounds in the table (16x16x8: a fifth round for 1.7 % of resets, a sixth for 0.4 %)
+#define M3_TS_ROUNDS 5
+#endif
 #ifndef M3_TS_INTERLEAVE
 #define M3_TS_INTERLEAVE 4
 #endif
@@ -1140,9 +1143,9 @@ constexpr bool RESET_TWO_STAGE = TwoStageOk<CF>::value;
 template <class CF>
 struct TwoStage {
     static constexpr int RB = __builtin_popcount(CF::TILE_MASK);  // raw bits per tile
-    static constexpr int ROUNDS = 4;
+    static constexpr int ROUNDS = M3_TS_ROUNDS;
     static constexpr int DRAWS = ROUNDS * CF::N;                  // 16x16x8: 1024
-    static_assert(DRAWS > 624 && DRAWS - 624 <= 624, "the first block and part of the second");
+    static_assert(DRAWS > 624 && DRAWS - 1248 <= 227, "two blocks and at most a first-phase head of a third");
     static constexpr int GROUPS = DRAWS / 64;
     static constexpr int RW = CF::W * RB;                         // table words per round
     static constexpr int TW = (ROUNDS * RW + 1 + 3) / 4 * 4;      // + mt[397], rows 16-B aligned
@@ -1161,8 +1164,8 @@ struct TwoStage {
 // keep the current block's values.
 template <int U, int NW = 624>
 __device__ __forceinline__ void wave_twist_u(uint32_t* key, int stride, int nu, int lane) {
-    static_assert(NW == 624 || (NW > 227 && NW <= 576), "a whole block, or a head of the next");
-    constexpr int E1 = NW < 227 ? NW : 227, E2 = NW == 624 ? 623 : NW;
+    static_assert(NW == 624 || NW <= 576, "a whole block, or a head of the next");
+    constexpr int E1 = NW < 227 ? NW : 227, E2 = NW == 624 ? 623 : (NW < 227 ? 227 : NW);
     for (int base = 0; base < E1; base += 64) {  // mt'[i] = mt[i+397] ^ twist(mt[i], mt[i+1])
         const int i = base + lane;
         uint32_t a0[U], a1[U], x[U];
@@ -1205,9 +1208,9 @@ __device__ __forceinline__ void wave_twist_u(uint32_t* key, int stride, int nu, 
 template <class CF>
 __global__ void __launch_bounds__(64) k_reset_stream(InitArgs a) {
     using TS = TwoStage<CF>;
-    constexpr int NX = TS::DRAWS - 624;  // words of the second block
+    constexpr int NX = TS::DRAWS <= 1248 ? TS::DRAWS - 624 : 624;  // words of the second block
     constexpr int G1 = 624 / 64;         // 64-draw groups wholly in the first block
-    static_assert(NX <= G1 * 64, "the second twist must leave the straddling group's first-block words");
+    static_assert(TS::DRAWS > 1248 || NX <= G1 * 64, "the second twist must leave the straddling group's words");
     constexpr int U = TS::U;
     __shared__ uint32_t key_s[TS::G * TS::KST];
     const int lane = (int)threadIdx.x;
@@ -1238,12 +1241,16 @@ __global__ void __launch_bounds__(64) k_reset_stream(InitArgs a) {
 #pragma unroll
             for (int u = 0; u < U; ++u) o0[u] = o1[u] = 0u;
             // draws 64g .. 64g + 63 into the row: one ballot per raw bit and board
-            auto pack = [&](int g) {
+            // (draw d sits at word d % 624 of the block last twisted, or of the one before it for the
+            // straddling group's low lanes -- words the twist of a block head leaves alone; `prev`:
+            // those words saved before a whole-block twist)
+            auto pack = [&](int g, const uint32_t* prev) {
                 const int d = g * 64 + lane;
-                const int w = d < 624 ? d : d - 624;  // (the straddling group: first-block words >= NX)
+                const bool low = prev && d % 624 >= 576;  // the previous block's words
                 uint32_t y[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) y[u] = mt_temper(key[u * TS::KST + w]) & CF::TILE_MASK;  // randint - 1
+                for (int u = 0; u < U; ++u)  // randint - 1
+                    y[u] = mt_temper(low ? prev[u] : key[u * TS::KST + d % 624]) & CF::TILE_MASK;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -1260,11 +1267,27 @@ __global__ void __launch_bounds__(64) k_reset_stream(InitArgs a) {
             };
             wave_twist_u<U>(key, TS::KST, nu, lane);  // draws 0 .. 623
 #pragma unroll 1
-            for (int g = 0; g < G1; ++g) pack(g);
+            for (int g = 0; g < G1; ++g) pack(g, 0);
             wave_sync();
-            wave_twist_u<U, NX>(key, TS::KST, nu, lane);  // draws 624 .. DRAWS - 1, over words [0, NX)
+            if constexpr (TS::DRAWS <= 1248) {
+                wave_twist_u<U, NX>(key, TS::KST, nu, lane);  // draws 624 .. DRAWS - 1, over words [0, NX)
 #pragma unroll 1
-            for (int g = G1; g < TS::GROUPS; ++g) pack(g);
+                for (int g = G1; g < TS::GROUPS; ++g) pack(g, 0);
+            } else {  // a whole second block and the head of a third
+                constexpr int G2 = 1248 / 64;  // groups below the third block's first word
+                uint32_t t9[U];                // the straddling group's first-block words (lanes < 48)
+#pragma unroll
+                for (int u = 0; u < U; ++u) t9[u] = key[u * TS::KST + (G1 * 64 + lane) % 624];
+                wave_sync();
+                wave_twist_u<U>(key, TS::KST, nu, lane);  // draws 624 .. 1247
+                pack(G1, t9);
+#pragma unroll 1
+                for (int g = G1 + 1; g < G2; ++g) pack(g, 0);
+                wave_sync();
+                wave_twist_u<U, TS::DRAWS - 1248>(key, TS::KST, nu, lane);  // draws 1248 .. DRAWS - 1
+#pragma unroll 1
+                for (int g = G2; g < TS::GROUPS; ++g) pack(g, 0);
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (u < nu) {
@@ -1960,6 +1983,10 @@ struct m3_env {
     uint32_t stride = 0;
     bool ready = false;  // every state field holds a board's state (m3_env_reset, or m3_env_set of each)
     uint32_t loaded = 0; // bit `what` per field m3_env_set has loaded since create (ready once all are)
+    // M3_ENV_LEGAL is derived from the boards: the step kernels write it only once a caller has
+    // asked for its device pointer (a device consumer reads it every step); m3_env_get computes it
+    // on request otherwise (20 B per board and step fewer writes)
+    bool legal_eager = false;
     bool stale = false;  // fields were loaded with m3_env_set: rederive() before the next step
     int8_t* boards[2] = {nullptr, nullptr};
     int cur = 0;
@@ -2164,7 +2191,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.trunc = e->trunc + o;
     a.flags = e->flags + o;
     a.draws = e->draws + o;
-    a.legal = e->legal + o * AW;
+    a.legal = e->legal_eager ? e->legal + o * AW : nullptr;
     a.packed = e->comm ? e->packed + (size_t)pb * e->n + o : nullptr;  // only the RCCL gather reads it
     a.counters = cnt;
     a.spill = e->spill + (size_t)s * KS<CF>::SPILL_RECORDS * LdsStore<CF, KS<CF>::GCAP, KS<CF>::B>::SPILL_WORDS;

@@ -166,7 +166,9 @@ int m3_env_step_device(m3_env *env, const int32_t *d_actions);
 #define M3_ENV_MOVES 5       /* int32 [n]  moves taken in the episode         */
 #define M3_ENV_FLAGS 6       /* uint32[n]  M3_FLAG_* of the last step         */
 #define M3_ENV_NEXT_ACTION 7 /* int32 [n]  pre-drawn seeded random action     */
-#define M3_ENV_LEGAL 8       /* uint32[n][words] legal bitset of the current board */
+#define M3_ENV_LEGAL 8       /* uint32[n][words] legal bitset of the current board (derived: m3_env_get
+                                computes it from the boards; after m3_env_device_ptr of this field every
+                                step writes it, for device consumers) */
 #define M3_ENV_SEEDS 9       /* uint32[n]  current episode seed               */
 #define M3_ENV_DRAWS 10      /* uint32[n]  raw MT draws of the last step      */
 #define M3_ENV_GATHERED 11   /* int32 [nranks][n] the env's all-gather buffer (after m3_env_comm_init) */

@@ -123,6 +123,28 @@ def test_c4_16x16_sample_vs_oracle():
     assert (e["final"] == o["final"]).all()
 
 
+@pytest.mark.parametrize("shape", [(9, 9, 6), (16, 16, 8)], ids=["9x9x6", "16x16x8"])
+def test_env_legal_sets_derived_and_eager(shape):
+    """M3_ENV_LEGAL is derived: m3_env_get computes it from the boards (lazy), and after
+    m3_env_device_ptr of it every step writes it (eager, for device consumers) -- through steps
+    autoresets (10-move episodes, 25 steps) both equal the stateless legal kernel on the boards."""
+    R, C, T = shape
+    n = 8192
+    lazy = BatchedMatch3Env(n, R, C, T, num_moves=10, env_goal=BIG, seed_base=3, autoreset=True, seed_stride=n)
+    eager = BatchedMatch3Env(n, R, C, T, num_moves=10, env_goal=BIG, seed_base=3, autoreset=True, seed_stride=n)
+    assert eager.device_ptr(_native.ENV_LEGAL) != 0
+    for t in range(25):
+        lazy.step()
+        eager.step()
+        if t % 4 == 3 or t == 24:
+            want = lazy.ctx.legal_bits(lazy.observations())
+            assert (lazy.legal_bits() == want).all(), t
+            assert (eager.observations() == lazy.observations()).all(), t
+            assert (eager.legal_bits() == want).all(), t
+    lazy.close()
+    eager.close()
+
+
 def test_c3_1m_boards_properties():
     """Config C3 size: 1,048,576 boards. Size-independent checks + a sampled oracle check."""
     n = 1 << 20
