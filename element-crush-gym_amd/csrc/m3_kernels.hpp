@@ -1755,14 +1755,27 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont_grid(E
     }
 }
 
+// k_env_fix runs on the step stream between two steps of a shard and almost never has work
+// (16x16x8: 7 recomputed boards in 50 steps of 262,144). At 512 VGPRs (16x16x8) its waves could only
+// start on a SIMD with no other wave resident, so each launch waited ~25 us for one to drain.
+// M3_FIX_LEAN: the specialised shapes run it one board per wave under a 128-VGPR bound (the rare
+// recompute spills to scratch; one active lane, so no divergence under the spills).
+#ifndef M3_FIX_LEAN
+#define M3_FIX_LEAN 1
+#endif
 template <class CF>
-__global__ void __launch_bounds__(FIX_BLOCK) k_env_fix(EnvArgs a) {
+constexpr uint32_t env_fix_lanes() { return (!CF::DYN && M3_FIX_LEAN) ? 1u : lanes_for<CF>(); }
+template <class CF>
+constexpr int ENV_FIX_WPS = (!CF::DYN && M3_FIX_LEAN) ? 4 : 1;
+
+template <class CF>
+__global__ void __launch_bounds__(FIX_BLOCK, ENV_FIX_WPS<CF>) k_env_fix(EnvArgs a) {
     const uint32_t cnt = a.counters[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], cnt);
     if (a.zero_next && blockIdx.x == 0 && threadIdx.x < 8) a.zero_next[threadIdx.x] = 0u;  // (CBLOCKS)
     const typename CF::Dim dm(a.shape);
-    for (uint32_t i = blockIdx.x * lanes_for<CF>() + threadIdx.x; threadIdx.x < lanes_for<CF>() && i < cnt;
-         i += gridDim.x * lanes_for<CF>()) {
+    constexpr uint32_t L = env_fix_lanes<CF>();
+    for (uint32_t i = blockIdx.x * L + threadIdx.x; threadIdx.x < L && i < cnt; i += gridDim.x * L) {
         const int64_t b = a.ovf_list[i];
         typename CF::Bd P[CF::NP];
         bytes_to_planes<CF>(a.cur + b * dm.cells(), P, dm);
@@ -2220,7 +2233,8 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         hipLaunchKernelGGL(k_env_cont_grid<CF>, dim3((unsigned)(g > 0 ? g : 1)), dim3(KS<CF>::B), 0, st, a);
         HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_env_fix<CF>, dim3(fix_grid<CF>()), dim3(FIX_BLOCK), 0, st, a);
+    // (one board per wave: 64 waves; else FIX_GRID x 64 lanes)
+    hipLaunchKernelGGL(k_env_fix<CF>, dim3(env_fix_lanes<CF>() == 1u ? 64 : fix_grid<CF>()), dim3(FIX_BLOCK), 0, st, a);
     HIP_TRY(hipGetLastError());
     if (timed) {  // the whole step pipeline of the shard, fixup pass included
         HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], st));
