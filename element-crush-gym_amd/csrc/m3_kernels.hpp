@@ -1756,12 +1756,14 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont_grid(E
 }
 
 // k_env_fix runs on the step stream between two steps of a shard and almost never has work
-// (16x16x8: 7 recomputed boards in 50 steps of 262,144). At 512 VGPRs (16x16x8) its waves could only
-// start on a SIMD with no other wave resident, so each launch waited ~25 us for one to drain.
-// M3_FIX_LEAN: the specialised shapes run it one board per wave under a 128-VGPR bound (the rare
-// recompute spills to scratch; one active lane, so no divergence under the spills).
+// (16x16x8: 7 recomputed boards in 50 steps of 262,144); at 512 VGPRs (16x16x8) its waves can only
+// start on a SIMD with no other wave resident (31 us average launch duration in the trace).
+// M3_FIX_LEAN=1: the specialised shapes run it one board per wave under a 128-VGPR bound (the rare
+// recompute spills to scratch; one active lane, so no divergence under the spills). Measured OFF:
+// 16x16x8 0.74-0.75 vs 0.80 G env-steps/s, 9x9 equal (gpurun_out/r05ac) -- the launch was not
+// what held the shard's stream.
 #ifndef M3_FIX_LEAN
-#define M3_FIX_LEAN 1
+#define M3_FIX_LEAN 0
 #endif
 template <class CF>
 constexpr uint32_t env_fix_lanes() { return (!CF::DYN && M3_FIX_LEAN) ? 1u : lanes_for<CF>(); }
