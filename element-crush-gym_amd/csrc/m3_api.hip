@@ -710,6 +710,8 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         constexpr size_t RW = 1 + EnvCont<decltype(cf)>::WORDS;
         if constexpr (K::CASCADE_LIMIT >= 0) alloc(&e->cont, RW * n * 4ull);
         if constexpr (RESET_TWO_STAGE<decltype(cf)>) alloc(&e->tab, (size_t)TwoStage<decltype(cf)>::TW * n * 4ull);
+        if constexpr (RESET_TWO_STAGE_REJ<decltype(cf)>)
+            alloc(&e->tab, (size_t)TwoStageRej<decltype(cf)>::TW * n * 4ull);
         return 0;
     });
     for (hipEvent_t& ev : e->gev)

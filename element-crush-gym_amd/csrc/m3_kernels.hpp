@@ -1378,6 +1378,8 @@ __global__ void __launch_bounds__(64) k_reset_tiles(InitArgs a) {
     }
 }
 
+#include "m3_reset9.hpp"
+
 // mt[397] of init_genrand(seeds[b]): the chain word of each board's current
 // episode (env resume, m3_env_set)
 __global__ void __launch_bounds__(256) k_mt397(int64_t n, const uint32_t* seeds, uint32_t* out) {
@@ -2104,6 +2106,21 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     int64_t g = (max_items + INIT_BLOCK - 1) / INIT_BLOCK;
     if (g > 4096) g = 4096;
     if constexpr (INIT_INLINE_FIX<CF>) {
+        if constexpr (RESET_TWO_STAGE_REJ<CF>) {
+            if (a.tab && a.defer) {  // 9x9x6 env prefetch (m3_reset9.hpp)
+                int64_t ga = (max_items + TwoStageRej<CF>::G - 1) / TwoStageRej<CF>::G;
+                ga = ga > 2048 ? 2048 : ga;
+                hipLaunchKernelGGL(k_reset_stream_rej<CF>, dim3((unsigned)ga), dim3(64), 0, stream, a);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_reset_tiles_rej<CF>, dim3((unsigned)g), dim3(64), 0, stream, a);
+                HIP_TRY(hipGetLastError());
+                int64_t gc = max_items / 64 + 1;  // the few past the table's rounds
+                gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+                hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
+                HIP_TRY(hipGetLastError());
+                return M3_OK;
+            }
+        }
         hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
         if (a.defer) {  // sized for the usual ~4 % deferred share, grid-strided
             HIP_TRY(hipGetLastError());
@@ -2161,6 +2178,7 @@ void prefetch_args(const m3_env* e, int64_t o, InitArgs& r) {
     r.slot_flags = e->ne_flags + o;
     r.cstride = e->n;
     if constexpr (RESET_TWO_STAGE<CF>) r.tab = e->tab ? e->tab + o * TwoStage<CF>::TW : nullptr;
+    if constexpr (RESET_TWO_STAGE_REJ<CF>) r.tab = e->tab ? e->tab + o * TwoStageRej<CF>::TW : nullptr;
 }
 
 // Enqueue one env step of shard s: on the step stream, wait for the prefetch

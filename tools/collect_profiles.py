@@ -28,8 +28,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = os.path.join(ROOT, "profiles")
 
 
-def last_json(path):
-    return json.loads(open(path).read().strip().splitlines()[-1])
+def last_json(path):  # (rocprofv3 logs its own lines after the bench line)
+    return json.loads([ln for ln in open(path).read().splitlines() if ln.startswith("{")][-1])
 
 
 bench = last_json(os.path.join(src, "bench.log"))
