@@ -15,7 +15,7 @@
 // match-mask loop over the rounds (funnel shifts out of the tile planes).
 // A reset needing more rounds than the table holds goes to k_init_coop.
 #ifndef M3_RESET9_TWO_STAGE
-#define M3_RESET9_TWO_STAGE 1
+#define M3_RESET9_TWO_STAGE 0
 #endif
 template <class CF, bool DYN = CF::DYN>
 struct TwoStageRejOk : std::false_type {};
