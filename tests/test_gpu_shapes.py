@@ -288,3 +288,40 @@ def test_frame_full_waves_episodes_and_rollouts_vs_oracle(shape):
     assert (ro["gain"] == want["gain"]).all() and (ro["steps"] == want["steps"]).all()
     assert (ro["draws"] == want["draws"]).all()
     ctx.close()
+
+
+def _has_match(b):
+    b = np.asarray(b)
+    h = (b[:, :-2] == b[:, 1:-1]) & (b[:, 1:-1] == b[:, 2:]) & (b[:, :-2] > 0)
+    v = (b[:-2, :] == b[1:-1, :]) & (b[1:-1, :] == b[2:, :]) & (b[:-2, :] > 0)
+    return bool(h.any() or v.any())
+
+
+def test_reset_cap_flag_reaches_callers_16x16x2():
+    """16x16x2 resets need 0.4 M - 7.5 M draws (oracle, seeds 1..8), past the 16,384-round cap for
+    most seeds: a reset stopped there returns a board that still has a match, and every caller must
+    see M3_FLAG_RESET_CAP -- m3_init_boards_ex's flags (m3_init_boards refuses with M3_ERR_CAP), and
+    the env's flags for an autoreset episode (the prefetched slot's flag)."""
+    R, C, T = 16, 16, 2
+    ctx = _native.Context(R, C, T)
+    seeds = np.arange(1, 65, dtype=np.uint32)
+    boards, draws, _, flags = ctx.init_boards(seeds, flags=True)
+    capped = (flags & _native.FLAG_RESET_CAP) != 0
+    assert capped.any() and (~capped).any()
+    assert [_has_match(b) for b in boards] == list(capped)
+    o = Oracle(R, C, T)
+    for i in np.nonzero(~capped)[0][:3]:  # the ones that finished: the reference's board
+        want, wdraws = o.init_board(int(seeds[i]))[:2]
+        assert (boards[i].reshape(-1) == want.reshape(-1)).all() and int(draws[i]) == int(wdraws)
+    with pytest.raises(_native.M3Error) as e:
+        ctx.init_boards(seeds)
+    assert e.value.code == -7  # M3_ERR_CAP
+    n = 64
+    env = BatchedMatch3Env(n, R, C, T, num_moves=1, env_goal=BIG, seed_base=1, autoreset=True, seed_stride=n)
+    for _ in range(2):
+        env.step()  # every episode is one move long: every board starts a new episode each step
+        obs = env.observations()
+        got = (env.flags() & _native.FLAG_RESET_CAP) != 0
+        assert [_has_match(b) for b in obs] == list(got)
+    env.close()
+    ctx.close()
