@@ -11,6 +11,8 @@ import socket
 import subprocess
 import sys
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -47,17 +49,19 @@ def test_bench_spawns_its_ranks_without_a_launcher():
     assert not any(x["torch_loaded"] for x in lines)  # the measurement path never imports torch
 
 
-def test_bench_gather_modes_two_ranks():
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_gather_modes_two_ranks(world):
     """--gather final (the N > 1 headline: one all-gather after the last timed step) and --gather step
-    (one per step), both inside the timed region: what each rank's timed loop enqueues, counted on a stub env."""
+    (one per step), both inside the timed region: what each rank's timed loop enqueues, counted on a stub env.
+    world 8: the driver's scaling configuration (8 spawned ranks, one rendezvous, no GPU touched)."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     for mode, want in (("final", 1), ("step", 3 + 1)):
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-               "--gather", mode, "--dry-rendezvous"]
-        out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "3", "--warmup",
+               "1", "--gather", mode, "--dry-rendezvous"]
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env, cwd=ROOT)
         assert out.returncode == 0, out.stderr[-3000:]
         lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
-        assert sorted(x["rank"] for x in lines) == [0, 1]
+        assert sorted(x["rank"] for x in lines) == list(range(world))
         assert all(x["gather"] == mode and x["stub_steps"] == 4 and x["stub_gathers"] == want for x in lines)
 
 
