@@ -367,6 +367,26 @@ __device__ __forceinline__ void block_copy_out(int8_t* __restrict__ g, const uin
     for (int i = (n16 << 4) + threadIdx.x; i < bytes; i += BLOCK) g[i] = (int8_t)lds[i];
 }
 
+// The staging copies with PAD bytes after every ROW-byte board in LDS (ROW % 16 == 0): 16-byte
+// chunks, each inside one row. A lane that reads or writes its own row then meets the other lanes
+// 4-way on a bank instead of 64-way (ROW = 256: every row would start on bank 0).
+template <int BLOCK, int ROW, int PAD>
+__device__ __forceinline__ void block_copy_in_rows(const int8_t* __restrict__ g, uint8_t* lds, int bytes) {
+    static_assert(ROW % 16 == 0 && PAD % 16 == 0, "whole 16-byte chunks");
+    const int n16 = bytes >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(g);
+    for (int i = threadIdx.x; i < n16; i += BLOCK)
+        *reinterpret_cast<uint4*>(lds + i * 16 + (i / (ROW / 16)) * PAD) = s4[i];
+}
+template <int BLOCK, int ROW, int PAD>
+__device__ __forceinline__ void block_copy_out_rows(int8_t* __restrict__ g, const uint8_t* lds, int bytes) {
+    static_assert(ROW % 16 == 0 && PAD % 16 == 0, "whole 16-byte chunks");
+    const int n16 = bytes >> 4;
+    uint4* d4 = reinterpret_cast<uint4*>(g);
+    for (int i = threadIdx.x; i < n16; i += BLOCK)
+        d4[i] = *reinterpret_cast<const uint4*>(lds + i * 16 + (i / (ROW / 16)) * PAD);
+}
+
 // N cell bytes (little-endian in cw[ceil(N/4)]) to dst of any alignment:
 // up to 3 head bytes, aligned dwords (one funnel shift each), up to 3 tail
 // bytes -- instead of N byte stores.
@@ -581,6 +601,9 @@ constexpr int PF_LAG = NSLOT - 1;   // steps between a prefetch and its first us
 // block of step t + PF_LAG + 1 (= step t's) is free and that kernel zeroes it -- no fill dispatch
 // per shard-step and no cross-block ticket.
 constexpr int CBLOCKS = PF_LAG + 1;
+#ifndef M3_STAGE_PAD  // k_env_step's 16x16 staging rows 16 B apart (bank conflicts, see block_copy_in_rows)
+#define M3_STAGE_PAD 1
+#endif
 
 // A reset launch processes "items". Item i is (board b, seed, slot): with a
 // list (env prefetch) b = list[i], seed = list_seed[i], slot = list_slot[i];
@@ -1645,7 +1668,9 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     // in between, so the two share storage (6 KB per wave at 9x9).
     using K = KS<CF>;
     static_assert(K::B == 64, "staging/table aliasing assumes one wave per workgroup");
-    constexpr int STAGE_WORDS = (K::B * CF::N + 16 + 3) / 4;
+    // 16x16: staging rows padded by 16 B (block_copy_in_rows)
+    constexpr int RPAD = (!CF::DYN && CF::N % 64 == 0 && M3_STAGE_PAD) ? 16 : 0;
+    constexpr int STAGE_WORDS = (K::B * (CF::N + RPAD) + 16 + 3) / 4;
     constexpr int TAB_WORDS = LdsStore<CF, K::GCAP, K::B>::WORDS;
     __shared__ __attribute__((aligned(16))) uint32_t stage_tab[STAGE_WORDS > TAB_WORDS ? STAGE_WORDS : TAB_WORDS];
     uint8_t* const lds = reinterpret_cast<uint8_t*>(stage_tab);
@@ -1654,7 +1679,8 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     const int NC = dm.cells();
     const int64_t b0 = (int64_t)blockIdx.x * KS<CF>::BPW;
     const int nb = (int)((a.n - b0) < KS<CF>::BPW ? (a.n - b0) : KS<CF>::BPW);
-    block_copy_in<KS<CF>::B>(a.cur + b0 * NC, lds, nb * NC);
+    if constexpr (RPAD) block_copy_in_rows<KS<CF>::B, CF::N, RPAD>(a.cur + b0 * NC, lds, nb * NC);
+    else block_copy_in<KS<CF>::B>(a.cur + b0 * NC, lds, nb * NC);
     const int t = threadIdx.x;
     const uint32_t cslot = t < nb ? a.slot[b0 + t] : 0u;
     lds_sync();
@@ -1674,14 +1700,14 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     if (t < nb) {
         const int64_t b = b0 + t;
         typename CF::Bd P[CF::NP];
-        lds_to_planes<CF>(lds, t, P, dm);  // (every lane of the wave, before any group-table write)
+        lds_to_planes<CF>(lds + t * RPAD, t, P, dm);  // (every lane of the wave, before any group-table write)
         typename K::Rng rng;
         rng.init(a.seeds[b], a.m397[(int64_t)cslot * a.cstride + b]);
         int r;
         uint32_t f;
         int res;
         // a finished step leaves its board bytes (or the next episode's) in its staging row
-        uint8_t* const row = lds + t * NC;
+        uint8_t* const row = lds + t * (NC + RPAD);
         if constexpr (K::CASCADE_LIMIT >= 0)  // (a.cont is set)
             res = env_step_one<CF, true>(P, a, b, rng, st, K::CASCADE_LIMIT, r, f, dm, row);
         else
@@ -1709,7 +1735,8 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
         }
     }
     lds_sync();
-    block_copy_out<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
+    if constexpr (RPAD) block_copy_out_rows<KS<CF>::B, CF::N, RPAD>(a.nxt + b0 * NC, lds, nb * NC);
+    else block_copy_out<KS<CF>::B>(a.nxt + b0 * NC, lds, nb * NC);
 #ifdef M3_PHASE_PROF
     if (live) st.end(0);
 #endif
