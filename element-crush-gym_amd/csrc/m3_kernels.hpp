@@ -91,7 +91,9 @@ template <class CF>
 struct KS {
     static constexpr int B = 64;
     static_assert(B == 64, "one-wave workgroups: lds_sync() orders a single wave's LDS accesses");
-    static constexpr int GCAP = 4;                  // match groups in LDS (more spill to a global pool)
+    // match groups in LDS per lane (more spill to a global pool): 9x9 6 (9 KB per wave, +0.8 %,
+    // gpurun_out/r05aj), 16x16 4 (past the staging area a larger table costs occupancy)
+    static constexpr int GCAP = CF::N <= 128 ? 6 : 4;
     // boards per wave: 64 (one per lane), but ONE for the 32 x 32 frame. Those kernels carry
     // ~2,500 SGPR spills through VGPR lanes, and with several lanes active some boards came out
     // wrong only in company (32x32x8 steps: 92 of 689; each exact alone) -- the lane interference
