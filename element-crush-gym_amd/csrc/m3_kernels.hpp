@@ -1667,7 +1667,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     // The board staging area is only live before the cascade (HBM -> LDS ->
     // planes) and after it (planes -> LDS -> HBM), the match-group table only
     // inside it; with one wave per workgroup nothing else can touch the LDS
-    // in between, so the two share storage (6 KB per wave at 9x9).
+    // in between, so the two share storage (9 KB per wave at 9x9: the 6-slot table).
     using K = KS<CF>;
     static_assert(K::B == 64, "staging/table aliasing assumes one wave per workgroup");
     // 16x16: staging rows padded by 16 B (block_copy_in_rows)
