@@ -106,15 +106,17 @@ def cpu_baseline(rows, cols, types, moves, goal, seconds):
 VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2
 
 
-def load_profile(shape_tag, boards, boards_per_launch):
-    """The committed rocprofv3 PMC summary of the step kernel (profiles/traffic_<shape>.json, or
-    profiles/traffic.json for the headline shape), if one matches this configuration."""
+def load_profile(shape_tag, boards, boards_per_launch, steps, warmup):
+    """The committed rocprofv3 summary of this configuration (profiles/traffic_<shape>.json, or
+    profiles/traffic.json for the headline shape; tools/collect_profiles.py), taken from the same
+    command line: shape, boards, shards, steps and warmup must all match, else {}."""
     for name in (f"traffic_{shape_tag}.json", "traffic.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 t = json.load(f)
             if (t.get("shape") == shape_tag and int(t.get("boards")) == boards
-                    and int(t.get("boards_per_launch", -1)) == boards_per_launch):
+                    and int(t.get("boards_per_launch", -1)) == boards_per_launch
+                    and int(t.get("steps", -1)) == steps and int(t.get("warmup", -1)) == warmup):
                 return t
         except Exception:
             pass
@@ -467,6 +469,7 @@ def main():
                                          return_local=True)
     rank_ms = dist.allgather_obj(elapsed_local / args.steps * 1e3) if dist else [elapsed_local / args.steps * 1e3]
     kms = env.kernel_ms()
+    kms_step = env.kernel_ms(step_kernel_only=True)
     stats = env.stats()
     # ---- after the clock: attest the run (nothing below is timed) ----
     nranks = env.comm_size()
@@ -492,41 +495,57 @@ def main():
     value = total_steps / elapsed
     step_s = elapsed / args.steps
     avg_kernel_s = float(kms.mean()) / 1e3 if len(kms) else float("nan")
+    avg_step_kernel_s = float(kms_step.mean()) / 1e3 if len(kms_step) else float("nan")
     # one launch of the step pipeline processes one shard (B / shards boards, contiguous, the last may be short)
     shard_boards = -(-B // stats["shards"])
-    bytes_per_launch = shard_boards * algorithmic_bytes_per_step(rows, cols)
-    achieved = bytes_per_launch / avg_kernel_s / 1e9
-    prof = load_profile(args.shape, B, shard_boards)
-    traffic = prof.get("hbm_bytes_per_launch")
+    alg = algorithmic_bytes_per_step(rows, cols)
+    bytes_per_launch = shard_boards * alg
+    prof = load_profile(args.shape, B, shard_boards, args.steps, args.warmup)
+    dom = prof.get("dominant")
+    # HBM roofline of the dominant kernel (k_env_step) in the contract's form: algorithmic bytes per
+    # launch (2RC + 21 per env-step) over its average launch duration, both live (HIP
+    # events on the shard's stream around k_env_step); traffic = the committed PMC pass's HBM bytes
     hbm = {
-        # one shard's step pipeline: k_env_step + k_env_cont (the continuation of the
-        # long cascades) + k_env_fix (dead boards, recomputes), bracketed by HIP events
-        # on the shard's stream
-        "kernel": "k_env_step + k_env_cont_grid + k_env_fix",
-        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-        "traffic": traffic, "algorithmic_bytes_per_launch": bytes_per_launch, "boards_per_launch": shard_boards,
-        "avg_kernel_ms": avg_kernel_s * 1e3,
-        # the shards' launches overlap, so per launch understates the whole GPU's rate
-        "aggregate_gbs": value / world * algorithmic_bytes_per_step(rows, cols) / 1e9,
-        "aggregate_frac": value / world * algorithmic_bytes_per_step(rows, cols) / 1e9 / HBM_PEAK_GBS,
-        "note": f"HBM roofline per BASELINE/SURVEY §8(d): {algorithmic_bytes_per_step(rows, cols)} B per "
-                f"{rows}x{cols} env-step (2RC + 21)"}
-    # The resource that binds is VALU issue: every kernel that runs inside a timed step (the step
-    # pipeline of each shard and the autoreset kernels beside it), wave64 VALU instructions per step
-    # from the committed PMC pass (profiles/traffic*.json, SQ_INSTS_VALU), over the step's wall time,
-    # against the chip's VALU issue peak.
-    vps = prof.get("valu_insts_per_step")
-    if vps:
+        "kernel": "k_env_step",
+        "achieved": bytes_per_launch / avg_step_kernel_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": bytes_per_launch / avg_step_kernel_s / 1e9 / HBM_PEAK_GBS,
+        "traffic": dom["hbm_bytes_per_launch"] if dom else None,
+        "traffic_bytes_per_board": dom["hbm_bytes_per_board"] if dom else None,
+        "algorithmic_bytes_per_launch": bytes_per_launch, "boards_per_launch": shard_boards,
+        "avg_kernel_ms": avg_step_kernel_s * 1e3,
+        "note": f"{alg} B per {rows}x{cols} env-step (2RC + 21); the path is integer VALU-bound, see roofline"}
+    pipeline = {
+        # one shard's whole step pipeline: k_env_step + k_env_cont_grid (the long cascades) + k_env_fix,
+        # bracketed by HIP events on the shard's stream
+        "kernels": "k_env_step + k_env_cont_grid + k_env_fix", "avg_ms": avg_kernel_s * 1e3,
+        "achieved_gbs": bytes_per_launch / avg_kernel_s / 1e9,
+        "traffic": prof.get("pipeline", {}).get("hbm_bytes_per_launch"),
+        "aggregate_gbs": value / world * alg / 1e9,
+        "aggregate_frac": value / world * alg / 1e9 / HBM_PEAK_GBS}
+    if dom:
+        # What binds: VALU issue. The dominant kernel's wave64 VALU instructions (committed PMC pass of
+        # this same command, profiles/<round>_dispatch.csv) against the chip's VALU issue peak: per step
+        # over the step's wall time (the two shards' launches overlap, so the per-launch quotient is
+        # about half the chip's rate), per launch over the live launch duration beside it; SIMT = active
+        # lanes per VALU instruction (SQ_THREAD_CYCLES_VALU / 64 SQ_ACTIVE_INST_VALU), lane_frac = frac x SIMT.
+        vw = dom["valu_insts_per_step"] / step_s
         roofline = {
-            "bound": "valu", "kernel": "whole step: " + " + ".join(vps["kernels"]),
-            "achieved": vps["total"] / step_s, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave64 VALU instr/s",
-            "frac": vps["total"] / step_s / VALU_PEAK_WAVE_INSTR_S,
-            "traffic": traffic, "valu_insts_per_step": vps, "ms_per_step": step_s * 1e3,
-            "how": "frac = valu_insts_per_step.total / (ms_per_step / 1e3) / peak; peak = 256 CUs x 4 SIMDs x "
-                   "2.4 GHz / 2 cycles per wave64 VALU instruction",
-            "source": prof.get("source"), "hbm": hbm}
+            "bound": "valu", "kernel": "k_env_step",
+            "achieved": vw, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave64 VALU instr/s",
+            "frac": vw / VALU_PEAK_WAVE_INSTR_S,
+            "frac_per_launch": dom["valu_insts_per_launch"] / avg_step_kernel_s / VALU_PEAK_WAVE_INSTR_S,
+            "simt": dom["simt"], "lane_frac": vw / VALU_PEAK_WAVE_INSTR_S * dom["simt"],
+            "traffic": dom["hbm_bytes_per_launch"],
+            "valu_insts_per_launch": dom["valu_insts_per_launch"], "valu_insts_per_step": dom["valu_insts_per_step"],
+            "wait_frac": dom["wait_frac"], "vmem_wr_per_wave": dom["vmem_wr_per_wave"],
+            "ms_per_step": step_s * 1e3,
+            "how": "frac = valu_insts_per_step / (ms_per_step / 1e3) / peak; frac_per_launch = valu_insts_per_launch "
+                   "/ hbm.avg_kernel_ms (live) / peak; peak = 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 "
+                   "VALU instruction; counts from " + prof.get("dispatch_csv", "?"),
+            "whole_step_frac": prof["valu_insts_per_step"]["total"] / step_s / VALU_PEAK_WAVE_INSTR_S,
+            "hbm": hbm, "pipeline": pipeline}
     else:
-        roofline = dict(hbm, bound="hbm", valu=None)
+        roofline = dict(hbm, bound="hbm", valu=None, hbm=hbm, pipeline=pipeline)
     out = {
         "metric": METRIC,
         "value": value,

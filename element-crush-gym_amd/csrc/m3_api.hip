@@ -707,7 +707,7 @@ int m3_env_create(m3_ctx* c, int64_t n, int num_moves, int env_goal, m3_env** ou
         using St = LdsStore<decltype(cf), K::GCAP, K::B>;
         alloc(&e->spill, (size_t)MAX_SHARDS * K::SPILL_RECORDS * St::SPILL_WORDS * 4);
         alloc(&e->m397, (size_t)NSLOT * n * 4ull);
-        constexpr size_t RW = 1 + EnvCont<decltype(cf)>::WORDS;
+        constexpr size_t RW = CONT_REC<decltype(cf)>;
         if constexpr (K::CASCADE_LIMIT >= 0) alloc(&e->cont, RW * n * 4ull);
         if constexpr (RESET_TWO_STAGE<decltype(cf)>) alloc(&e->tab, (size_t)TwoStage<decltype(cf)>::TW * n * 4ull);
         if constexpr (RESET_TWO_STAGE_REJ<decltype(cf)>)
@@ -1164,7 +1164,7 @@ int m3_env_timing(m3_env* e, int capacity) {
     HIP_TRY(hipSetDevice(e->ctx->device));
     int rc = sync_env(e);
     if (rc) return rc;
-    while ((int)e->tev.size() < 2 * capacity) {
+    while ((int)e->tev.size() < 3 * capacity) {
         hipEvent_t ev;
         HIP_TRY(hipEventCreate(&ev));
         e->tev.push_back(ev);
@@ -1180,7 +1180,18 @@ int m3_env_kernel_ms(m3_env* e, float* out_ms, int max_n, int* out_n) {
     const int n = e->tn < max_n ? e->tn : max_n;
     int rc = sync_env(e);
     if (rc) return rc;
-    for (int i = 0; i < n; ++i) HIP_TRY(hipEventElapsedTime(&out_ms[i], e->tev[2 * i], e->tev[2 * i + 1]));
+    for (int i = 0; i < n; ++i) HIP_TRY(hipEventElapsedTime(&out_ms[i], e->tev[3 * i], e->tev[3 * i + 2]));
+    *out_n = n;
+    return M3_OK;
+}
+
+int m3_env_step_kernel_ms(m3_env* e, float* out_ms, int max_n, int* out_n) {
+    CHECK_ARG(e && out_n && (max_n == 0 || out_ms), "bad arguments");
+    HIP_TRY(hipSetDevice(e->ctx->device));
+    const int n = e->tn < max_n ? e->tn : max_n;
+    int rc = sync_env(e);
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i) HIP_TRY(hipEventElapsedTime(&out_ms[i], e->tev[3 * i], e->tev[3 * i + 1]));
     *out_n = n;
     return M3_OK;
 }

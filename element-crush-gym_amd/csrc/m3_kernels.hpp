@@ -71,6 +71,13 @@ constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 #define M3_RESET_KCAP 454
 #endif
 constexpr uint32_t RESET_KCAP = M3_RESET_KCAP;
+// grid caps of the env-prefetch reset kernels (0: sized by the queue's usual length), see launch_init
+#ifndef M3_PF_GRID
+#define M3_PF_GRID 0
+#endif
+#ifndef M3_PF_COOP_GRID
+#define M3_PF_COOP_GRID 0
+#endif
 // 16x16x8 resets: 1 = lane-per-board on the two-block register chain (k_init_chain2),
 // 0 = lane-per-board FullMT in scratch (k_init_fix_lane)
 #ifndef M3_RESET16_CHAIN2
@@ -866,7 +873,11 @@ __device__ uint32_t wave_reset(const InitArgs& a, int64_t item, uint32_t* key, u
 // Reset on the register-only MT19937 chain; grid-strided over n (or *list_count).
 // A reset that needs >= 624 draws (~0.7 % at 9x9x6) is redone by its own wave
 // right away (wave_reset).
-template <class CF>
+// REDO: the explicit-reset form, whose wave redoes its >= 624-draw resets itself (wave_reset, 2.5 KB
+// of LDS for the MT state); the env prefetch (a.defer) defers them to k_init_coop instead and leaves
+// that LDS out, so with the tile ring its wave takes ~14 KB -- what a CU full of k_env_step waves
+// (16 x 9 KB) still has free.
+template <class CF, bool REDO>
 __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
     const int64_t cnt = a.list_count ? (int64_t)*a.list_count : a.n;
     if (a.stats && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.stats[0], (uint32_t)cnt);
@@ -884,8 +895,8 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
     NoStore* const pp = nullptr;
 #endif
     static_assert(INIT_INLINE_FIX<CF> && INIT_BLOCK == 64, "the in-wave redo is one wave's");
-    __shared__ uint32_t key_s[624];
-    __shared__ __attribute__((aligned(16))) uint8_t cell_s[(CF::N + 3) / 4 * 4 + 16];
+    __shared__ uint32_t key_s[REDO ? 624 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t cell_s[REDO ? (CF::N + 3) / 4 * 4 + 16 : 16];
     for (int64_t base = (int64_t)blockIdx.x * INIT_BLOCK; base < cnt; base += (int64_t)gridDim.x * INIT_BLOCK) {
         const int64_t i = base + threadIdx.x;
         bool ok = true;
@@ -902,7 +913,7 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
 #endif
         }
         uint64_t bad = __ballot(!ok);
-        if (a.defer) {  // left to k_init_coop: one wave-aggregated append
+        if (!REDO) {  // left to k_init_coop: one wave-aggregated append (a.defer is set)
             if (bad) {
                 const int lane = (int)threadIdx.x;
                 uint32_t base = 0;
@@ -914,10 +925,12 @@ __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
         }
         // this wave redoes its >= 624-draw resets at once
         if (bad && a.stats && threadIdx.x == 0) atomicAdd(&a.stats[1], (uint32_t)__builtin_popcountll(bad));
-        while (bad) {
-            const int l = __builtin_ctzll(bad);
-            bad &= bad - 1ull;
-            wave_reset<CF>(a, __shfl(i, l), key_s, cell_s, (int)threadIdx.x);
+        if constexpr (REDO) {
+            while (bad) {
+                const int l = __builtin_ctzll(bad);
+                bad &= bad - 1ull;
+                wave_reset<CF>(a, __shfl(i, l), key_s, cell_s, (int)threadIdx.x);
+            }
         }
     }
 #ifdef M3_PHASE_PROF
@@ -1481,7 +1494,7 @@ struct EnvArgs {
     uint32_t* pf_slot;
     const uint32_t* m397;  // [NSLOT][cstride] mt[397] of each slot's seed
     int64_t cstride;
-    uint32_t* cont;        // nullable: continuation records of paused steps (k_env_cont_grid), [1 + WORDS][cont_stride]
+    uint32_t* cont;        // nullable: continuation records of paused steps (k_env_cont_grid), CONT_REC words each
     int64_t cont_stride;
     uint32_t* zero_next;   // the counter block of the next step, zeroed by k_env_fix (see CBLOCKS)
 };
@@ -1489,115 +1502,145 @@ struct EnvArgs {
 using m3k::EnvArgs;
 namespace {
 
+// Counter block words (8 per shard and step, see CBLOCKS): the continuation count and the
+// prefetch queue length share one 64-bit word, so k_env_step's wave takes both of its slots with
+// ONE atomic (low half: continuation records, high half: queue entries).
+enum : int { CNT_OVF = 0, CNT_PF_DEFER = 2, CNT_SPILL = 3, CNT_CONT = 4, CNT_PF = 5 };
+
 // Match3Env.step bookkeeping (env.py:48-56) after BoardV2.apply_action (r, f,
 // HL/VL of the resulting board), and the same-step autoreset (the finished
 // step's reward/done/flags stay visible, the observation and episode state
 // become the next episode's). mv / sc0: the board's moves and score before the
-// step. Returns false if the next random action ran past the RNG (recompute);
-// nothing has been stored then.
+// step. In three parts, so k_env_step can take the queue slots of its resets and
+// the continuation records of its paused lanes with one atomic between the
+// decisions and the stores:
+//   env_fin_begin   the decisions (draw count, next seeded random action, done /
+//                   truncated, autoreset) and every load the stores need (the next
+//                   episode's slot -- first action, reset flags, legal set, cells);
+//                   false if the next random action ran past the RNG (recompute;
+//                   nothing has been stored then);
+//   env_fin_store   the per-board stores and the reset swap;
+//   env_fin_queue   the freed slot's entry in the prefetch queue (slot q).
+// env_finish is the three in a row with its own queue atomic (k_env_cont_grid,
+// k_env_fix).
 //
-// Memory order of the tail: every load it needs (the next episode's slot --
-// first action, legal set, cells -- and the lane's seed and slot) and the
-// prefetch-queue atomic are issued BEFORE its first store. A wave's vector
-// memory counter retires in issue order, so a load issued behind stores is
-// only usable once those stores are acknowledged too; written load / store /
-// load / store (the legal-set copy of the next episode), the wave paid one
-// full memory round trip per word (round-5 phase profile: 42 % of k_env_step's
-// wave cycles in this block, profiles/r05a_phase9.log).
+// Memory order: every load and the atomic are issued BEFORE the first store. A
+// wave's vector memory counter covers loads and stores, so a value returned behind
+// stores is only usable once those stores are acknowledged too (round 5: one full
+// memory round trip per load / store pair; round 6: the continuation atomic, issued
+// after the step's stores, waited for all of them).
 // row (nullable, k_env_step): the board's bytes go to this LDS staging row --
 // the resulting board, or the next episode's cells on a reset -- and P is not
 // needed afterwards. Without a row, P holds the board to write (the next
 // episode's on a reset).
-template <class CF, class RNG, class Store>
-__device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
-                                           int r, uint32_t f, const typename CF::Bd& HL, const typename CF::Bd& VL,
-                                           int mv, int sc0, const typename CF::Dim& dm, uint8_t* row = nullptr) {
-    const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
-    const int sc = sc0 + r;
-    const int mv1 = mv + 1;
-    const int tr = sc >= a.goal;                        // env.py:53
-    const int dn = tr || mv1 == a.num_moves;            // env.py:54
-    const uint32_t ndraws = stepped ? rng.draws() : 0u;  // the step's own draws (before the next action's)
+template <class CF>
+struct EnvFin {
+    static constexpr bool CELLS_IN_REGS = !CF::DYN;  // frame boards load their cells at the use
+    static constexpr int NWS = (CF::N + 3) / 4;
+    uint32_t ndraws, f, nflags, s_old, seed;
+    int r, tr, dn, sc, mv1, na, first;
+    bool reset;
+    int64_t ob;
     uint32_t act[CF::AW];
-    action_bits<CF>(HL, VL, act, dm);
-    int na = -1;
-    if (stepped) {
-        na = random_action<CF>(act, rng);
-        if (rng.overflow) return false;
-        if (na < 0) f |= FLAG_NO_LEGAL;
-    }
-    mark<PH_NEXT>(st);
-    const bool reset = dn && a.autoreset;
-    if (row) planes_to_bytes<CF>(P, row, dm);  // (LDS) P is dead from here on in k_env_step
-    mark<PH_TBYTES>(st);
-    // ---- loads: everything the stores below need ----
-    constexpr bool CELLS_IN_REGS = !CF::DYN;    // frame boards load their cells at the use
-    constexpr int NWS = (CF::N + 3) / 4;
-    const int NW = cell_words<CF>(dm);
-    const int AW = dm.aw();
-    uint32_t s_old = 0u, seed = 0u;
-    int64_t ob = 0;
-    int first = -1;
-    uint32_t nflags = 0u;  // the next episode's reset flags (FLAG_RESET_CAP)
     uint32_t lg[CF::AW];
     uint32_t cw[CELLS_IN_REGS ? NWS : 1];
-    if (reset) {  // swap in the prefetched next episode (slot + 1)
-        s_old = a.slot[b];
-        seed = a.seeds[b] + a.stride;
+};
+
+template <class CF, class RNG, class Store>
+__device__ __forceinline__ bool env_fin_begin(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
+                                              int r, uint32_t f, const typename CF::Bd& HL, const typename CF::Bd& VL,
+                                              int mv, int sc0, const typename CF::Dim& dm, uint8_t* row,
+                                              EnvFin<CF>& e, const uint32_t* known_slot = nullptr,
+                                              const uint32_t* known_seed = nullptr, bool cells = true) {
+    const bool stepped = !(f & (FLAG_TERMINAL | FLAG_BAD_ACTION));
+    e.r = r;
+    e.sc = sc0 + r;
+    e.mv1 = mv + 1;
+    e.tr = e.sc >= a.goal;                          // env.py:53
+    e.dn = e.tr || e.mv1 == a.num_moves;            // env.py:54
+    e.ndraws = stepped ? rng.draws() : 0u;          // the step's own draws (before the next action's)
+    action_bits<CF>(HL, VL, e.act, dm);
+    e.na = -1;
+    if (stepped) {
+        e.na = random_action<CF>(e.act, rng);
+        if (rng.overflow) return false;
+        if (e.na < 0) f |= FLAG_NO_LEGAL;
+    }
+    e.f = f;
+    mark<PH_NEXT>(st);
+    e.reset = e.dn && a.autoreset;
+    if (row) planes_to_bytes<CF>(P, row, dm);  // (LDS) P is dead from here on in k_env_step
+    mark<PH_TBYTES>(st);
+    // ---- loads: everything the stores need ----
+    const int AW = dm.aw();
+    e.s_old = 0u;
+    e.seed = 0u;
+    e.ob = 0;
+    e.first = -1;
+    e.nflags = 0u;  // the next episode's reset flags (FLAG_RESET_CAP)
+    if (e.reset) {  // swap in the prefetched next episode (slot + 1)
+        // (k_env_step passes the slot and seed it loaded before the cascade: no load, then a
+        // dependent load of the slot's words, on the way to the stores)
+        const uint32_t s_old = known_slot ? *known_slot : a.slot[b];
+        e.seed = (known_seed ? *known_seed : a.seeds[b]) + a.stride;
         const uint32_t s_new = s_old + 1u == (uint32_t)NSLOT ? 0u : s_old + 1u;
-        ob = (int64_t)s_new * a.cstride + b;  // slots are strided by the env's n
-        first = a.ne_first[ob];
-        nflags = a.ne_flags ? a.ne_flags[ob] : 0u;
+        e.ob = (int64_t)s_new * a.cstride + b;  // slots are strided by the env's n
+        e.first = a.ne_first[e.ob];
+        e.nflags = a.ne_flags ? a.ne_flags[e.ob] : 0u;
         if (a.legal) {
 #pragma unroll
-            for (int i = 0; i < CF::AW; ++i) lg[i] = i < AW ? a.ne_legal[ob * AW + i] : 0u;
+            for (int i = 0; i < CF::AW; ++i) e.lg[i] = i < AW ? a.ne_legal[e.ob * AW + i] : 0u;
         }
-        if constexpr (CELLS_IN_REGS) {
+        if constexpr (EnvFin<CF>::CELLS_IN_REGS) {
+            if (cells) {
 #pragma unroll
-            for (int q = 0; q < NWS; ++q) cw[q] = a.ne_words[ob * NWS + q];
+                for (int q = 0; q < EnvFin<CF>::NWS; ++q) e.cw[q] = a.ne_words[e.ob * EnvFin<CF>::NWS + q];
+            }
         }
-        s_old = s_new;  // (from here on: the new slot)
+        e.s_old = s_new;  // (from here on: the new slot)
     }
     prof_drain(st);
     mark<PH_TLOAD>(st);
-    // the freed slot is queued for the episode after next: one atomic per wave, not per lane
-    const uint64_t m = __ballot(reset);
-    uint32_t qbase = 0u;
-    int leader = 0;
-    if (m) {
-        leader = __ffsll((unsigned long long)m) - 1;
-        if ((int)__lane_id() == leader) qbase = atomicAdd(&a.counters[1], (uint32_t)__popcll(m));
-    }
-    prof_drain(st);
-    mark<PH_TATOM>(st);
-    // ---- stores ----
-    a.draws[b] = ndraws;
-    a.reward[b] = r;
-    a.trunc[b] = (uint8_t)tr;
-    a.done[b] = (uint8_t)dn;
-    a.flags[b] = f | nflags;  // (a reset that stopped at its round cap flags the step that swapped it in)
-    if (a.packed) a.packed[b] = (r << 2) | (tr << 1) | dn;
-    if (!reset) {
-        a.score[b] = sc;
-        a.moves[b] = mv1;
-        a.next_action[b] = na;
-        if (a.legal) store_legal<CF>(a.legal + b * AW, act, dm);
+    return true;
+}
+
+template <class CF, class Store>
+__device__ __forceinline__ void env_fin_store(typename CF::Bd* P, const EnvArgs& a, int64_t b, Store& st,
+                                              const EnvFin<CF>& e, const typename CF::Dim& dm, uint8_t* row,
+                                              bool cells = true) {
+    const int AW = dm.aw();
+    a.draws[b] = e.ndraws;
+    a.reward[b] = e.r;
+    a.trunc[b] = (uint8_t)e.tr;
+    a.done[b] = (uint8_t)e.dn;
+    a.flags[b] = e.f | e.nflags;  // (a reset that stopped at its round cap flags the step that swapped it in)
+    if (a.packed) a.packed[b] = (e.r << 2) | (e.tr << 1) | e.dn;
+    if (!e.reset) {
+        a.score[b] = e.sc;
+        a.moves[b] = e.mv1;
+        a.next_action[b] = e.na;
+        if (a.legal) store_legal<CF>(a.legal + b * AW, e.act, dm);
     } else {
-        a.slot[b] = (uint8_t)s_old;
-        a.seeds[b] = seed;
+        a.slot[b] = (uint8_t)e.s_old;
+        a.seeds[b] = e.seed;
         a.score[b] = 0;
         a.moves[b] = 0;
-        a.next_action[b] = first;
+        a.next_action[b] = e.first;
         if (a.legal) {
 #pragma unroll
             for (int i = 0; i < CF::AW; ++i)
-                if (i < AW) a.legal[b * AW + i] = lg[i];
+                if (i < AW) a.legal[b * AW + i] = e.lg[i];
         }
-        if constexpr (CELLS_IN_REGS) {
-            if (row) store_cells<CF::N>(row, cw);
-            else planes_from_words<CF>(cw, P);
+        if constexpr (EnvFin<CF>::CELLS_IN_REGS) {
+            if (!cells) {
+                // (k_env_step with M3_COOP_CELLS: the wave copies them, coop_reset_cells)
+            } else if (row) {
+                store_cells<CF::N>(row, e.cw);
+            } else {
+                planes_from_words<CF>(e.cw, P);
+            }
         } else {
-            const uint8_t* src = reinterpret_cast<const uint8_t*>(a.ne_words + ob * NW);
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(a.ne_words + e.ob * cell_words<CF>(dm));
             if (row) {
                 for (int x = 0; x < dm.cells(); ++x) row[x] = src[x];
             } else {
@@ -1606,15 +1649,73 @@ __device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a,
         }
     }
     mark<PH_RESET>(st);
-    if (m) {
-        const int lane = (int)__lane_id();
-        qbase = __shfl(qbase, leader);
-        if (reset) {
-            const uint32_t q = qbase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            a.pf_list[q] = (uint32_t)b;
-            a.pf_seed[q] = seed + (uint32_t)(NSLOT - 1) * a.stride;
-            a.pf_slot[q] = s_old == 0u ? (uint32_t)(NSLOT - 1) : s_old - 1u;
+}
+
+// the freed slot (the one before the new current slot) takes the episode NSLOT - 1 ahead
+__device__ __forceinline__ void env_fin_queue(const EnvArgs& a, int64_t b, uint32_t q, uint32_t seed, uint32_t s_new) {
+    a.pf_list[q] = (uint32_t)b;
+    a.pf_seed[q] = seed + (uint32_t)(NSLOT - 1) * a.stride;
+    a.pf_slot[q] = s_new == 0u ? (uint32_t)(NSLOT - 1) : s_new - 1u;
+}
+
+// The next episode's cells of the wave's resetting lanes (mask m), copied into their LDS staging
+// rows by the whole wave: NWS lanes per board, one dword each (64 / NWS boards per pass), instead of
+// NWS words in every lane's registers across the atomic (M3_COOP_CELLS). ob: the lane's slot word
+// offset (EnvFin::ob). Loads of every pass first, then the byte writes.
+#ifndef M3_COOP_CELLS
+#define M3_COOP_CELLS 1
+#endif
+template <class CF>
+__device__ __forceinline__ void coop_reset_cells(const EnvArgs& a, uint64_t m, int64_t ob, uint8_t* lds, int row_stride) {
+    constexpr int NWS = EnvFin<CF>::NWS, PER = 64 / NWS;
+    const int lane = (int)__lane_id(), j = lane / NWS, w = lane - j * NWS;
+    while (m) {
+        int src = 0;
+        uint64_t mm = m;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {  // this lane's board of the pass: the j-th set lane of m
+            const int l = mm ? __ffsll((unsigned long long)mm) - 1 : -1;
+            if (k == j) src = l;
+            if (mm) mm &= mm - 1ull;
         }
+        const int64_t sob = __shfl(ob, src < 0 ? 0 : src);
+        uint32_t v = 0u;
+        if (j < PER && src >= 0) v = a.ne_words[sob * NWS + w];
+        if (j < PER && src >= 0) {
+            uint8_t* dst = lds + src * row_stride + 4 * w;
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+                if (4 * w + y < CF::N) dst[y] = (uint8_t)(v >> (8 * y));
+        }
+        m = mm;
+    }
+}
+
+// rank of this lane among the set lanes of m
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+}
+
+template <class CF, class RNG, class Store>
+__device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
+                                           int r, uint32_t f, const typename CF::Bd& HL, const typename CF::Bd& VL,
+                                           int mv, int sc0, const typename CF::Dim& dm, uint8_t* row = nullptr) {
+    EnvFin<CF> e;
+    if (!env_fin_begin<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm, row, e)) return false;
+    // the freed slot is queued for the episode after next: one atomic per wave, not per lane
+    const uint64_t m = __ballot(e.reset);
+    uint32_t qbase = 0u;
+    int leader = 0;
+    if (m) {
+        leader = __ffsll((unsigned long long)m) - 1;
+        if ((int)__lane_id() == leader) qbase = atomicAdd(&a.counters[CNT_PF], (uint32_t)__popcll(m));
+    }
+    prof_drain(st);
+    mark<PH_TATOM>(st);
+    env_fin_store<CF>(P, a, b, st, e, dm, row);
+    if (m) {
+        qbase = __shfl(qbase, leader);
+        if (e.reset) env_fin_queue(a, b, qbase + lane_rank(m), e.seed, e.s_old);
     }
     mark<PH_QUEUE>(st);
     return true;
@@ -1656,11 +1757,47 @@ __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a
 }
 
 // Continuation records of paused steps (KS::CASCADE_LIMIT): word 0 the
-// shard-local board index, words 1.. the Cont state; word w of record q at
-// cont[w * cont_stride + q] (consecutive records of a wave are consecutive
-// dwords). cont_count (the step's counter block [4]) counts them.
+// shard-local board index, words 1.. the Cont state, padded to CONT_REC words
+// (9x9x6: 32 words, 128 B) so a lane writes and reads its record with 16-byte
+// accesses -- 8 instructions each way instead of one per word (round 5 wrote them
+// SoA, word w of record q at cont[w * n + q]: 31 stores per wave). Record q at
+// cont[q * CONT_REC]; the step's counter block [CNT_CONT] counts them.
 template <class CF>
 using EnvCont = Cont<CF, typename KS<CF>::Rng>;
+template <class CF>
+constexpr int CONT_REC = (1 + EnvCont<CF>::WORDS + 3) & ~3;
+
+template <class CF>
+__device__ __forceinline__ void cont_store(uint32_t* rec, uint32_t b, const typename CF::Bd* P,
+                                           const typename KS<CF>::Rng& rng, int r, uint32_t f) {
+    constexpr int RW = CONT_REC<CF>;
+    uint32_t w[RW];
+    w[0] = b;
+    EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t x) { w[i + 1] = x; });
+#pragma unroll
+    for (int i = 1 + EnvCont<CF>::WORDS; i < RW; ++i) w[i] = 0u;
+    uint4* d = reinterpret_cast<uint4*>(rec);
+#pragma unroll
+    for (int k = 0; k < RW / 4; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+
+template <class CF>
+__device__ __forceinline__ int64_t cont_load(const uint32_t* rec, typename CF::Bd* P, typename KS<CF>::Rng& rng,
+                                             int& r, uint32_t& f) {
+    constexpr int RW = CONT_REC<CF>;
+    uint32_t w[RW];
+    const uint4* s = reinterpret_cast<const uint4*>(rec);
+#pragma unroll
+    for (int k = 0; k < RW / 4; ++k) {
+        const uint4 v = s[k];
+        w[4 * k] = v.x;
+        w[4 * k + 1] = v.y;
+        w[4 * k + 2] = v.z;
+        w[4 * k + 3] = v.w;
+    }
+    EnvCont<CF>::load(P, rng, r, f, [&](int i) { return w[i + 1]; });
+    return (int64_t)w[0];
+}
 
 template <class CF>
 __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArgs a) {
@@ -1697,8 +1834,10 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     LdsStore<CF, KS<CF>::GCAP, KS<CF>::B> st{as_lds(gtab + t)};
 #endif
     st.spill = a.spill;
-    st.pool_next = &a.counters[3];
+    st.pool_next = &a.counters[CNT_SPILL];
     st.pool_cap = K::SPILL_RECORDS;
+    bool reset_lane = false;  // (M3_COOP_CELLS: the wave copies the resetting lanes' next cells below)
+    int64_t reset_ob = 0;
     if (t < nb) {
         const int64_t b = b0 + t;
         typename CF::Bd P[CF::NP];
@@ -1710,31 +1849,81 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
         int res;
         // a finished step leaves its board bytes (or the next episode's) in its staging row
         uint8_t* const row = lds + t * (NC + RPAD);
-        if constexpr (K::CASCADE_LIMIT >= 0)  // (a.cont is set)
-            res = env_step_one<CF, true>(P, a, b, rng, st, K::CASCADE_LIMIT, r, f, dm, row);
-        else
+        if constexpr (K::CASCADE_LIMIT >= 0) {  // (a.cont is set)
+            // env_step_one<CF, true> with the epilogue split round one atomic per wave: the
+            // decisions of every lane (paused, or finished and resetting), then the wave's
+            // continuation records and prefetch queue entries in one 64-bit atomicAdd, then the
+            // stores (see env_finish)
+            const int act_in = a.actions ? a.actions[b] : a.next_action[b];
+            const int mv = a.moves[b];
+            const int sc0 = a.score[b];
+            typename CF::Bd HL, VL;
+            res = ENV_STEP_DONE;
+            if (apply_begin<CF>(P, a.num_moves - mv, act_in, rng, f, HL, VL, st, r, dm)) {
+                const int c =
+                    apply_cascade_ex<CF, CASX_STOP_DEAD>(P, rng, f, HL, VL, st, r, K::CASCADE_LIMIT, false, dm);
+                if (!(f & FLAG_RECOMPUTE)) {
+                    if (c == CAS_PAUSED) {
+                        res = ENV_STEP_PAUSED;
+                    } else if (c == CAS_DEAD) {
+                        f |= FLAG_CONT_DEAD;
+                        res = ENV_STEP_PAUSED;
+                    }
+                }
+            }
+            if (f & FLAG_RECOMPUTE) res = ENV_STEP_RECOMPUTE;
+            EnvFin<CF> e;
+            const uint32_t seed_in = rng.seed;
+            if (res == ENV_STEP_DONE &&
+                !env_fin_begin<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm, row, e, &cslot, &seed_in, !M3_COOP_CELLS))
+                res = ENV_STEP_RECOMPUTE;
+            const bool fin = res == ENV_STEP_DONE, paused = res == ENV_STEP_PAUSED;
+            const bool reset = fin && e.reset;
+            const uint64_t mp = __ballot(paused), mr = __ballot(reset);
+            uint32_t cbase = 0u, qbase = 0u;
+            int leader = 0;
+            if (mp | mr) {
+                leader = __ffsll((unsigned long long)(mp | mr)) - 1;
+                if ((int)__lane_id() == leader) {
+                    const unsigned long long add =
+                        (unsigned long long)__popcll(mp) | ((unsigned long long)__popcll(mr) << 32);
+                    const unsigned long long old =
+                        atomicAdd(reinterpret_cast<unsigned long long*>(&a.counters[CNT_CONT]), add);
+                    cbase = (uint32_t)old;
+                    qbase = (uint32_t)(old >> 32);
+                }
+            }
+            if (res == ENV_STEP_RECOMPUTE) {  // (rare; its row is rewritten by k_env_fix)
+                const uint32_t slot = atomicAdd(&a.counters[CNT_OVF], 1u);
+                a.ovf_list[slot] = (uint32_t)b;
+            }
+            prof_drain(st);
+            mark<PH_TATOM>(st);
+            if (fin) env_fin_store<CF>(P, a, b, st, e, dm, row, !M3_COOP_CELLS);
+            reset_lane = reset;
+            reset_ob = e.ob;
+            if (mp | mr) {
+                cbase = __shfl(cbase, leader);
+                qbase = __shfl(qbase, leader);
+                if (reset) env_fin_queue(a, b, qbase + lane_rank(mr), e.seed, e.s_old);
+                // paused steps leave a continuation record; their rows are rewritten by k_env_cont_grid
+                // (round 6 A/B: the record at the board's own index before the atomic and only the index
+                // in the compacted list -- equal speed, one more dependent load in k_env_cont_grid)
+                if (paused)
+                    cont_store<CF>(a.cont + (int64_t)(cbase + lane_rank(mp)) * CONT_REC<CF>, (uint32_t)b, P, rng, r, f);
+            }
+            mark<PH_QUEUE>(st);
+        } else {
             res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f, dm, row);
-        if (res == ENV_STEP_RECOMPUTE) {  // (its row is rewritten by k_env_fix)
-            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
-            a.ovf_list[slot] = (uint32_t)b;
-        }
-        // paused steps leave a continuation record (one atomic per wave); their rows are
-        // rewritten by k_env_cont_grid
-        const bool paused = res == ENV_STEP_PAUSED;
-        const uint64_t m = K::CASCADE_LIMIT >= 0 ? __ballot(paused) : 0ull;
-        if (m) {
-            const int lane = (int)__lane_id(), leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&a.counters[4], (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            if (paused) {
-                const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                uint32_t* rec = a.cont + q;
-                const int64_t cs = a.cont_stride;
-                rec[0] = (uint32_t)b;
-                EnvCont<CF>::save(P, rng, r, f, [&](int i, uint32_t w) { rec[(int64_t)(i + 1) * cs] = w; });
+            if (res == ENV_STEP_RECOMPUTE) {  // (its row is rewritten by k_env_fix)
+                const uint32_t slot = atomicAdd(&a.counters[CNT_OVF], 1u);
+                a.ovf_list[slot] = (uint32_t)b;
             }
         }
+    }
+    if constexpr (K::CASCADE_LIMIT >= 0 && M3_COOP_CELLS && !CF::DYN) {
+        const uint64_t mr = __ballot(reset_lane);  // (all 64 lanes: a ragged last wave too)
+        if (mr) coop_reset_cells<CF>(a, mr, reset_ob, lds, NC + RPAD);
     }
     lds_sync();
     if constexpr (RPAD) block_copy_out_rows<KS<CF>::B, CF::N, RPAD>(a.nxt + b0 * NC, lds, nb * NC);
@@ -1756,20 +1945,17 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont_grid(E
     // the other shard's step waves and the resets: issue first (A/B: within noise).
     __builtin_amdgcn_s_setprio(3);
     __shared__ uint32_t tab[LdsStore<CF, K::GCAP, K::B>::WORDS];
-    const uint32_t cnt = a.counters[4];
+    const uint32_t cnt = a.counters[CNT_CONT];
     LdsStore<CF, K::GCAP, K::B> st{as_lds(tab + threadIdx.x)};
     st.spill = a.spill;
-    st.pool_next = &a.counters[3];
+    st.pool_next = &a.counters[CNT_SPILL];
     st.pool_cap = K::SPILL_RECORDS;
-    const int64_t cs = a.cont_stride;
     for (uint32_t q = blockIdx.x * K::B + threadIdx.x; q < cnt; q += gridDim.x * K::B) {
-        const uint32_t* rec = a.cont + q;
-        const int64_t b = rec[0];
         typename CF::Bd P[CF::NP];
         typename K::Rng rng;
         int r;
         uint32_t f;
-        EnvCont<CF>::load(P, rng, r, f, [&](int i) { return rec[(int64_t)(i + 1) * cs]; });
+        const int64_t b = cont_load<CF>(a.cont + (int64_t)q * CONT_REC<CF>, P, rng, r, f);
         const int mv = a.moves[b], sc0 = a.score[b];
         typename CF::Bd HL, VL;
         const bool dead = (f & FLAG_CONT_DEAD) != 0;  // settled with no legal move: continue at the shuffle
@@ -1778,7 +1964,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::CONT_WPS) k_env_cont_grid(E
         apply_cascade_ex<CF, 0>(P, rng, f, HL, VL, st, r, -1, dead, dm);
         const bool ok = !(f & FLAG_RECOMPUTE) && env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm);
         if (!ok) {
-            const uint32_t slot = atomicAdd(&a.counters[0], 1u);
+            const uint32_t slot = atomicAdd(&a.counters[CNT_OVF], 1u);
             a.ovf_list[slot] = (uint32_t)b;
         } else {
             planes_to_bytes<CF>(P, reinterpret_cast<uint8_t*>(a.nxt + b * dm.cells()), dm);
@@ -1803,7 +1989,7 @@ constexpr int ENV_FIX_WPS = (!CF::DYN && M3_FIX_LEAN) ? 4 : 1;
 
 template <class CF>
 __global__ void __launch_bounds__(FIX_BLOCK, ENV_FIX_WPS<CF>) k_env_fix(EnvArgs a) {
-    const uint32_t cnt = a.counters[0];
+    const uint32_t cnt = a.counters[CNT_OVF];
     if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&a.stats[0], cnt);
     if (a.zero_next && blockIdx.x == 0 && threadIdx.x < 8) a.zero_next[threadIdx.x] = 0u;  // (CBLOCKS)
     const typename CF::Dim dm(a.shape);
@@ -2048,9 +2234,9 @@ struct m3_env {
     hipEvent_t upload_ev[2] = {nullptr, nullptr};
     bool upload_pend[2] = {false, false};  // upload_ev[p] recorded and not yet waited on by the host
     bool upload_this = false;              // the step being enqueued reads actions[step & 1]
-    // counters, 64 words per shard: [8q + 0] step overflow count, [8q + 1]
-    // prefetch queue length, [8q + 2] deferred prefetch resets, [8q + 3] spill
-    // records taken, [8q + 4] continuation records (q = step % CBLOCKS); stats
+    // counters, 64 words per shard: [8q + CNT_*] (q = step % CBLOCKS): step overflow count,
+    // deferred prefetch resets, spill records taken, continuation records | prefetch queue
+    // length (one 64-bit word); stats
     // [40] step recomputes, [41] resets, [42] reset recomputes; [48 + k] the
     // reset / slot-fill overflow counts (shard 0's block)
     uint32_t* counters = nullptr;
@@ -2064,7 +2250,7 @@ struct m3_env {
     uint32_t* ne_legal = nullptr;
     uint32_t* ne_flags = nullptr;  // [NSLOT][n] M3_FLAG_RESET_CAP of each slot's reset
     uint32_t* m397 = nullptr;  // [NSLOT][n]
-    uint32_t* cont = nullptr;  // continuation records of paused steps [1 + EnvCont::WORDS][n] (k_env_cont_grid)
+    uint32_t* cont = nullptr;  // continuation records of paused steps [n][CONT_REC] (k_env_cont_grid)
     uint32_t* defer = nullptr; // prefetch resets k_init leaves to k_init_coop [n]
     uint32_t* tab = nullptr;   // two-stage reset table rows [n][TwoStage::TW] (16x16x8)
     // prefetch queues and their overflow lists, by step % PF_LAG
@@ -2134,6 +2320,11 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     if (max_items == 0) return M3_OK;
     int64_t g = (max_items + INIT_BLOCK - 1) / INIT_BLOCK;
     if (g > 4096) g = 4096;
+    // env prefetch (a.defer): the reset kernels grid-stride over the queue, and their waves share the
+    // CUs with the step kernels (k_init holds 21.5 KB of LDS per wave, two and a half step waves'
+    // worth); capping their grids bounds how many run at once. The queue is needed PF_LAG steps later.
+    const int64_t pf_cap = a.defer ? (int64_t)M3_PF_GRID : 0, coop_cap = a.defer ? (int64_t)M3_PF_COOP_GRID : 0;
+    if (pf_cap > 0 && g > pf_cap) g = pf_cap;
     if constexpr (INIT_INLINE_FIX<CF>) {
         if constexpr (RESET_TWO_STAGE_REJ<CF>) {
             if (a.tab && a.defer) {  // 9x9x6 env prefetch (m3_reset9.hpp)
@@ -2145,16 +2336,19 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
                 HIP_TRY(hipGetLastError());
                 int64_t gc = max_items / 64 + 1;  // the few past the table's rounds
                 gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+                if (coop_cap > 0 && gc > coop_cap) gc = coop_cap;
                 hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
                 HIP_TRY(hipGetLastError());
                 return M3_OK;
             }
         }
-        hipLaunchKernelGGL(k_init<CF>, dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
+        if (a.defer) hipLaunchKernelGGL((k_init<CF, false>), dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
+        else hipLaunchKernelGGL((k_init<CF, true>), dim3((unsigned)g), dim3(INIT_BLOCK), 0, stream, a);
         if (a.defer) {  // sized for the usual ~4 % deferred share, grid-strided
             HIP_TRY(hipGetLastError());
             int64_t gc = max_items / 16 + 1;
             gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+            if (coop_cap > 0 && gc > coop_cap) gc = coop_cap;
             hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
         }
     } else if constexpr (!CF::DYN && M3_RESET16_CHAIN2) {  // 16x16x8: ~60 % of resets need the second MT block
@@ -2170,12 +2364,14 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
             const InitArgs& s = a;
             int64_t ga = (max_items + TwoStage<CF>::G - 1) / TwoStage<CF>::G;
             ga = ga > 2048 ? 2048 : ga;
+            if (pf_cap > 0 && ga > pf_cap) ga = pf_cap;
             hipLaunchKernelGGL(k_reset_stream<CF>, dim3((unsigned)ga), dim3(64), 0, stream, s);
             HIP_TRY(hipGetLastError());
             hipLaunchKernelGGL(k_reset_tiles<CF>, dim3((unsigned)(g > 4096 ? 4096 : g)), dim3(64), 0, stream, s);
             HIP_TRY(hipGetLastError());
             int64_t gc = max_items / 32 + 1;  // the ~2 % past the table's rounds
             gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+            if (coop_cap > 0 && gc > coop_cap) gc = coop_cap;
             hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
         }
     } else {  // frame shapes: FullMT (lane-private scratch); 32 x 32 frame: one board per wave
@@ -2269,13 +2465,14 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     a.pf_slot = e->pf_slot[par] + o;
     a.m397 = e->m397 + o;
     a.cstride = e->n;
-    a.cont = KS<CF>::CASCADE_LIMIT >= 0 ? e->cont + o : nullptr;
-    a.cont_stride = e->n;
+    a.cont = KS<CF>::CASCADE_LIMIT >= 0 ? e->cont + o * CONT_REC<CF> : nullptr;
+    a.cont_stride = CONT_REC<CF>;
     a.zero_next = base + 8 * ((e->steps + 1) % CBLOCKS);
     const bool timed = e->tn < e->tcap;
-    if (timed) HIP_TRY(hipEventRecord(e->tev[2 * e->tn], st));
+    if (timed) HIP_TRY(hipEventRecord(e->tev[3 * e->tn], st));
     hipLaunchKernelGGL(k_env_step<CF>, dim3(grid_for<CF>(sh.n)), dim3(KS<CF>::B), 0, st, a);
     HIP_TRY(hipGetLastError());
+    if (timed) HIP_TRY(hipEventRecord(e->tev[3 * e->tn + 1], st));  // k_env_step alone (the dominant kernel)
     if constexpr (KS<CF>::CASCADE_LIMIT >= 0) {
         // grid-strides over the device-side count of paused steps: sized for their usual share (~20 % at limit 2)
         const int64_t g = ((int64_t)(sh.n * 0.25) + KS<CF>::B - 1) / KS<CF>::B;
@@ -2286,7 +2483,7 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
     hipLaunchKernelGGL(k_env_fix<CF>, dim3(env_fix_lanes<CF>() == 1u ? 64 : fix_grid<CF>()), dim3(FIX_BLOCK), 0, st, a);
     HIP_TRY(hipGetLastError());
     if (timed) {  // the whole step pipeline of the shard, fixup pass included
-        HIP_TRY(hipEventRecord(e->tev[2 * e->tn + 1], st));
+        HIP_TRY(hipEventRecord(e->tev[3 * e->tn + 2], st));
         e->tn++;
     }
     HIP_TRY(hipEventRecord(sh.ev, st));
@@ -2301,11 +2498,11 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
         r.list = e->pf_list[par] + o;
         r.list_seed = e->pf_seed[par] + o;
         r.list_slot = e->pf_slot[par] + o;
-        r.list_count = &cnt[1];
+        r.list_count = &cnt[CNT_PF];
         r.stats = base + 41;
         if constexpr (INIT_INLINE_FIX<CF> || (!CF::DYN && M3_RESET16_CHAIN2) || RESET_TWO_STAGE<CF>) {
             r.defer = e->defer + o;
-            r.defer_count = &cnt[2];  // zeroed with the block
+            r.defer_count = &cnt[CNT_PF_DEFER];  // zeroed with the block
         }
         prefetch_args<CF>(e, o, r);
         // the grid is sized for the expected number of finished boards and grid-strides

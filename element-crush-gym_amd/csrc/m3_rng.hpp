@@ -70,6 +70,13 @@ struct ChainMTT {
         seed = s;
         mt397 = s397;
         overflow = 0;
+#ifndef __HIP_DEVICE_COMPILE__
+        // b_* / c_* are only read after slow() set them (draws 227 / 454), but a paused step copies
+        // the whole struct into its Cont record (m3_rules.hpp); the host build defines them so
+        // MemorySanitizer sees no copy of an unset word (tests/hostcore msan). The device code
+        // leaves them unset: zeroing would hold 4 more VGPRs from the first draw on.
+        b_lo = b_hi = c_lo = c_hi = 0u;
+#endif
         reseed();
     }
     M3_HD void reseed() {

@@ -770,8 +770,51 @@ M3_HD int match_scan(const typename CF::Bd* P, typename CF::Bd& mask, typename C
     return MATCH_FOUND;
 }
 
+// get_matches without the per-start loop when that is provably equal (round 6). If no cell lies in
+// both a horizontal and a vertical run of three or more, the scan visits exactly the first cell of
+// every maximal run (a first cell can only be covered by a run of the other direction), takes that
+// run whole and never merges (a run meets no earlier group): every maximal run is its own group,
+// the mask is the union of the runs, and a group's length is its run's. Spawns (groups longer than
+// 3): an h-run of 4 puts V, of 5 M, at its first cell + 2; a v-run of 4 puts H, of 5 M, two rows
+// below its top (boardFunctions.py:159-169, get_center :8-13 on a sorted straight run). Runs of 6 or
+// more (centre past + 2) and crossing runs (L / T groups, merged arms, duplicates) take the scan.
+// Whole-board operations only: no loop, no group table, no overflow. Host-checked equal to the scan
+// on every fixture and on random boards (tests/test_hostcore_cpu.py::test_fast_matches_equal_scan).
+#ifndef M3_FAST_MATCH
+#define M3_FAST_MATCH 1
+#endif
 template <class CF, class Store>
 M3_HD int get_matches(const typename CF::Bd* P, typename CF::Bd& mask, typename CF::Bd* sw, Store& st) {
+    if constexpr (M3_FAST_MATCH) {
+        using Bd = typename CF::Bd;
+        using G = typename CF::G;
+        constexpr int C = CF::C, R = CF::R;
+        constexpr Bd CLE2 = G::col_le(C - 2), RLE2 = G::row_le(R - 2);
+        const Bd nz = tb_nonzero<CF>(P);
+        const Bd e1h = CLE2 & tb_eq<CF, 1>(P);   // TB[x] == TB[x+1], same row
+        const Bd e1v = RLE2 & tb_eq<CF, C>(P);   // TB[x] == TB[x+C]
+        const Bd h3 = nz & e1h & at<1>(e1h);     // a horizontal triple starts here
+        const Bd v3 = nz & e1v & at<C>(e1v);     // a vertical triple starts here
+        if (!(h3 | v3).any()) {
+            mask = Bd::zero();
+            sw[0] = sw[1] = sw[2] = Bd::zero();
+            return MATCH_NONE;
+        }
+        const Bd hc = h3 | at<-1>(h3) | at<-2>(h3);      // every cell of a horizontal run
+        const Bd vc = v3 | at<-C>(v3) | at<-2 * C>(v3);  // every cell of a vertical run
+        const Bd h4 = h3 & at<1>(h3), v4 = v3 & at<C>(v3);  // a run of >= 4 starts here
+        const bool six = (h4 & at<2>(h4)).any() || (v4 & at<2 * C>(v4)).any();
+        if (!(hc & vc).any() && !six) {
+            const Bd hf = h4.andnot(at<-1>(e1h));          // first cells of h-runs of 4 or 5
+            const Bd vf = v4.andnot(at<-C>(e1v));          // top cells of v-runs of 4 or 5
+            const Bd hf5 = hf & at<2>(h3), vf5 = vf & at<2 * C>(v3);
+            mask = hc | vc;
+            sw[0] = at<-2 * C>(vf.andnot(vf5));                // H (v-run of 4)
+            sw[1] = at<-2>(hf.andnot(hf5));                    // V (h-run of 4)
+            sw[2] = at<-2>(hf5) | at<-2 * C>(vf5);             // M (runs of 5)
+            return MATCH_FOUND;
+        }
+    }
     return match_scan<CF, true>(P, mask, sw, st);
 }
 
@@ -1460,10 +1503,17 @@ M3_HD void init_board(typename CF::Bd* P, RNG& mt, S& st, const typename CF::Dim
 // the first MT block, 624): the caller recomputes it. `draws` = raw outputs
 // consumed by __init__.
 // --------------------------------------------------------------------------
+// The stream is kept as a RING of TWMAX plane words (round 6; was the whole 624-tile stream, 21
+// words): a round only reads its own N tiles, and every live lane of a wave is at the same round, so
+// a lane's unread tiles span about N + one 64-draw chunk + the acceptance spread between lanes (9x9:
+// ~150-250 tiles of the 16-word ring's 384 usable). A lane whose unread tiles would overrun the ring
+// stops (its reset reports the cap: the exact fallback redoes it), so the ring never loses a tile.
+// At 9x9 this halves k_init's LDS (tm: 16 KB -> 12 KB per wave).
 template <class CF>
 struct TileGen {
-    static constexpr int TWMAX = 21;  // 624 tiles at most, + funnel pad
-    static constexpr int MAXR = 624 / CF::N + 2;  // rounds one MT block can feed
+    static constexpr int TWMAX = CF::N <= 128 ? 16 : 32;  // ring words per plane (a power of two)
+    static constexpr int MAXR = 624 / CF::N + 2;         // rounds one MT block can feed
+    static_assert((TWMAX & (TWMAX - 1)) == 0, "ring index by mask");
 };
 
 
@@ -1481,6 +1531,9 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
 #pragma unroll
     for (int p = 0; p < CF::BITS; ++p) cur[p] = 0u;
     uint32_t nt = 0u, accw = 0u;
+    uint32_t floor_tile = 0u;  // first tile this lane still has to read (its current round's)
+    bool ring_full = false;    // the unread tiles would overrun the ring (the reset goes to the fallback)
+    constexpr uint32_t RING_TILES = 32u * (uint32_t)(TW - CF::W - 1);  // (take reads W + 1 words)
     // Every lane draws raw outputs [g.k, kend): the trip count is the same on
     // all lanes (one draw per trip), so the MT19937 chain runs without
     // divergence; tiles are appended to the lane's own stream. pos[r] records
@@ -1498,7 +1551,8 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
                     accw = 0u;
                 }
             }
-            if (ok && nt < (uint32_t)(32 * TW)) {
+            if (ok && nt - floor_tile >= RING_TILES) ring_full = true;
+            if (ok && !ring_full) {
                 const uint32_t val = t + 1u, sh = nt & 31u;
 #pragma unroll
                 for (int p = 0; p < CF::BITS; ++p) cur[p] |= ((val >> p) & 1u) << sh;
@@ -1506,35 +1560,34 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
                 if ((nt & 31u) == 0u) {
 #pragma unroll
                     for (int p = 0; p < CF::BITS; ++p) {
-                        tm[(p * TW + (int)(nt >> 5) - 1) * stride] = cur[p];
+                        tm[(p * TW + (int)(((nt >> 5) - 1u) & (uint32_t)(TW - 1))) * stride] = cur[p];
                         cur[p] = 0u;
                     }
                 }
                 if (nt % (uint32_t)N == 0u && nt / (uint32_t)N < (uint32_t)MAXR) pos[(nt / N) * stride] = k + 1u;
             }
         }
-        if ((nt >> 5) < (uint32_t)TW) {  // the partial word, so a round can read it
 #pragma unroll
-            for (int p = 0; p < CF::BITS; ++p) tm[(p * TW + (int)(nt >> 5)) * stride] = cur[p];
-        }
+        for (int p = 0; p < CF::BITS; ++p)  // the partial word, so a round can read it
+            tm[(p * TW + (int)((nt >> 5) & (uint32_t)(TW - 1))) * stride] = cur[p];
     };
     // make sure every lane that still needs them has `need` tiles (or the block is exhausted)
     auto ensure = [&](uint32_t need, bool want) {
-        while (wave_any(want && nt < need) && g.k < kcap) {
+        while (wave_any(want && !ring_full && nt < need) && g.k < kcap) {
             const uint32_t kend = g.k + 64u < kcap ? g.k + 64u : kcap;
             gen_to(kend);
         }
         return !want || nt >= need;
     };
     auto take = [&](uint32_t j, Bd* T) {  // tiles [j, j + N) as planes
-        const int q = (int)(j >> 5);
+        const uint32_t q = j >> 5;
         const uint32_t sh = j & 31u;
 #pragma unroll
         for (int p = 0; p < CF::BITS; ++p) {
-            uint32_t lo = tm[(p * TW + q) * stride];
+            uint32_t lo = tm[(p * TW + (int)(q & (uint32_t)(TW - 1))) * stride];
 #pragma unroll
             for (int i = 0; i < CF::W; ++i) {
-                const uint32_t hi = (q + i + 1 < TW) ? tm[(p * TW + q + i + 1) * stride] : 0u;
+                const uint32_t hi = tm[(p * TW + (int)((q + (uint32_t)i + 1u) & (uint32_t)(TW - 1))) * stride];
                 T[p].w[i] = sh ? ((lo >> sh) | (hi << (32u - sh))) : lo;
                 lo = hi;
             }
@@ -1546,6 +1599,7 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
     for (int p = 0; p < CF::NP; ++p) P[p] = Bd::zero();
     bool ok = ensure((uint32_t)N, true);                       // :21
     if (ok) take(0u, P);
+    floor_tile = (uint32_t)N;
     if constexpr (HasProf<S>::value) ps->template mark<PH_REFILL>();
     uint32_t rounds = 1u;
     bool live = ok;
@@ -1565,6 +1619,9 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
 #pragma unroll
             for (int p = 0; p < CF::BITS; ++p) P[p] = P[p].andnot(mask) | (T[p] & mask);
             ++rounds;
+            floor_tile = rounds * (uint32_t)N;  // (earlier tiles are never read again)
+        } else {
+            floor_tile = nt;  // (a finished lane reads nothing more: no ring limit)
         }
         if constexpr (HasProf<S>::value) ps->template mark<PH_REFILL>();
     }

@@ -40,7 +40,7 @@ EXPORTS = [
     "m3_env_step_device", "m3_env_get", "m3_env_set", "m3_env_device_ptr",
     "m3_comm_unique_id", "m3_env_comm_init", "m3_env_comm_size", "m3_env_gather", "m3_env_gather_device", "m3_env_debug_stall",
     "m3_env_stats", "m3_env_timing",
-    "m3_env_kernel_ms",
+    "m3_env_kernel_ms", "m3_env_step_kernel_ms",
 ]
 
 
@@ -105,6 +105,7 @@ def lib():
             "m3_env_stats": ([vp, vp], i32),
             "m3_env_timing": ([vp, i32], i32),
             "m3_env_kernel_ms": ([vp, vp, i32, vp], i32),
+            "m3_env_step_kernel_ms": ([vp, vp, i32, vp], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name, None)  # (an older A/B build may lack newer entry points;

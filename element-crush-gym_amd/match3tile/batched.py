@@ -109,12 +109,14 @@ class BatchedMatch3Env:
         """Record HIP events around the next `capacity` step-kernel launches."""
         check(lib().m3_env_timing(self.handle, int(capacity)))
 
-    def kernel_ms(self) -> np.ndarray:
-        """Per-launch durations (ms) of the step kernel since enable_timing()."""
+    def kernel_ms(self, step_kernel_only: bool = False) -> np.ndarray:
+        """Per-launch durations (ms) of each shard's step pipeline (k_env_step .. k_env_fix) since
+        enable_timing(); step_kernel_only: of k_env_step alone."""
         cap = 1 << 16
         out = np.empty(cap, np.float32)
         n = ctypes.c_int(0)
-        check(lib().m3_env_kernel_ms(self.handle, ptr(out), cap, ctypes.byref(n)))
+        fn = lib().m3_env_step_kernel_ms if step_kernel_only else lib().m3_env_kernel_ms
+        check(fn(self.handle, ptr(out), cap, ctypes.byref(n)))
         return out[: n.value].copy()
 
     def stats(self) -> dict:

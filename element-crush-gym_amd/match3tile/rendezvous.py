@@ -80,6 +80,7 @@ class RendezvousServer:
 
     def _serve(self):
         conns = [None] * self.world
+        extra = []  # a rejected connection (bad or duplicate rank): it gets the error frame too
         try:
             self.sock.settimeout(self.timeout)
             for _ in range(self.world):
@@ -87,6 +88,7 @@ class RendezvousServer:
                 c.settimeout(self.timeout)
                 rank = int(_recv(c).decode())
                 if not 0 <= rank < self.world or conns[rank] is not None:
+                    extra.append(c)
                     raise ValueError(f"rendezvous: bad or duplicate rank {rank}")
                 conns[rank] = c
             while True:
@@ -102,14 +104,15 @@ class RendezvousServer:
         except Exception as e:  # surfaced to the clients: an error frame, then a closed connection
             self.error = e
             msg = _HDR.pack(_ERR) + f"{type(e).__name__}: {e}".encode()
-            for c in conns:
+            for c in conns + extra:
                 if c is not None:
                     try:
                         _send(c, msg)
+                        c.shutdown(socket.SHUT_WR)  # the frame goes out before the close (no RST over unread data)
                     except OSError:
                         pass
         finally:
-            for c in conns:
+            for c in conns + extra:
                 if c is not None:
                     c.close()
             self.sock.close()

@@ -221,11 +221,14 @@ int m3_env_stats(m3_env *env, uint64_t out[4]);
 
 /* ---- timing helpers for bench.py ---------------------------------------- */
 /* Kernel-side timing: after m3_env_timing(env, cap), each of the next cap
- * m3_env_step calls records a HIP event pair on the env stream around the
- * step kernel (k_env_step). m3_env_kernel_ms waits for the last pair and
- * returns the per-launch durations in ms (out_n of them). */
+ * shard-step launches records HIP events on its shard's stream before
+ * k_env_step, after it, and after the pipeline's last kernel (k_env_cont_grid,
+ * k_env_fix). m3_env_kernel_ms waits for them and returns the per-launch
+ * durations of the whole pipeline in ms (out_n of them); m3_env_step_kernel_ms
+ * the same for k_env_step alone (the dominant kernel, bench.py's roofline). */
 int m3_env_timing(m3_env *env, int capacity);
 int m3_env_kernel_ms(m3_env *env, float *out_ms, int max_n, int *out_n);
+int m3_env_step_kernel_ms(m3_env *env, float *out_ms, int max_n, int *out_n);
 
 #ifdef __cplusplus
 }

@@ -29,7 +29,7 @@ static int fail(const char* what, int cfg, long i) {
 
 // one configuration: cfg id (0, 1 or FRAME after hc_set_frame), board R x C, T types, BITS
 static int run(int cfg, int R, int C, int T, int BITS, uint32_t& rs, long& checks) {
-    const long n = 96;
+    const long n = getenv("HC_N") ? atol(getenv("HC_N")) : 96;  // (the MemorySanitizer run uses fewer)
     const int N = R * C, A = R * (C - 1) * 2, AW = (A + 31) / 32;
     const int TM = (1 << BITS) - 1, H = TM + 1, V = 2 * H, STM = (1 << (BITS + 1)) + 1 + TM, M = TM + STM + 1;
     std::vector<uint32_t> seeds(n), m397(n);
@@ -79,6 +79,19 @@ static int run(int cfg, int R, int C, int T, int BITS, uint32_t& rs, long& check
     std::vector<int32_t> rounds(n);
     hc_rounds(cfg, n, boards.data(), seeds.data(), na.data(), act.data(), rounds.data());
     for (int k = 0; k < 700; k += 37) (void)hc_chain_draw(seeds[k % n], k);
+    {   // MCTS.rollout as k_rollout's rollout_one composes the rules (the round-4/5 lane-interference
+        // path): 1 and 20 moves from the stepped boards; n_actions 1 must equal the one step + choice
+        std::vector<uint32_t> rsd(n), dr(n), fg(n);
+        std::vector<int32_t> gain(n), steps(n);
+        for (long i = 0; i < n; ++i) rsd[i] = lcg(&rs);
+        for (int k : {1, 20}) {
+            std::vector<int32_t> nk(n, k);
+            hc_rollout(cfg, n, out.data(), seeds.data(), nk.data(), rsd.data(), gain.data(), steps.data(), dr.data(),
+                       fg.data());
+            for (long i = 0; i < n; ++i)
+                if (gain[i] >= 0 && steps[i] > k) return fail("rollout steps", cfg, i);
+        }
+    }
     checks += n;
     return 0;
 }
@@ -89,12 +102,14 @@ int main() {
     if (run(0, 9, 9, 6, 3, rs, checks)) return 1;
     if (run(1, 16, 16, 8, 4, rs, checks)) return 1;
     static const int frames[][3] = {{3, 3, 3}, {5, 3, 3}, {7, 7, 4}, {10, 8, 5}, {12, 12, 7}, {16, 3, 4},
-                                    {6, 5, 15}, {9, 9, 2}, {9, 9, 6}};
+                                    {6, 5, 15}, {9, 9, 2}, {9, 9, 6}, {10, 8, 9}};
     for (const auto& f : frames) {
         if (hc_set_frame(f[0], f[1], f[2]) != 0) return 1;
         int bits = 0;
         while ((1 << bits) <= f[2]) ++bits;
         if (run(FRAME, f[0], f[1], f[2], bits, rs, checks)) return 1;
+        printf("frame %dx%dx%d done\n", f[0], f[1], f[2]);
+        fflush(stdout);
     }
     printf("hostcore asan: %ld boards through every entry point, no sanitizer report\n", checks);
     return 0;

@@ -10,6 +10,7 @@
 // 9x9x6 / 16x16x8.
 #include "../../element-crush-gym_amd/csrc/m3_rules.hpp"
 
+#include <stdlib.h>
 #include <string.h>
 
 using namespace m3;
@@ -301,8 +302,70 @@ static void rounds_n(long n, const int8_t* boards, const uint32_t* seeds, const 
     }
 }
 
+// MCTS.rollout (mctslib/standard/mcts.py:14-19) the way k_rollout's rollout_one runs it: the first
+// choice on the rollout seed's chain, every step and later choice on the step seed's chain. Writes
+// gain, steps, draws (global-stream position when the rollout ends), flags; -1 gain when the chain
+// ran out (the kernel's k_rollout_fix replay).
+template <class CF>
+static void rollout_n(long n, const int8_t* boards, const uint32_t* seeds, const int32_t* nact, const uint32_t* rseeds,
+                      int32_t* gain, int32_t* steps, uint32_t* draws, uint32_t* flags) {
+    const auto dm = make_dim<CF>();
+    for (long i = 0; i < n; ++i) {
+        typename CF::Bd P[CF::NP], HL, VL;
+        load_planes<CF>(boards + i * dm.cells(), P, dm);
+        ChainMT first, rng;
+        first.init(rseeds[i], mt_state397(rseeds[i]));
+        rng.init(seeds[i], mt_state397(seeds[i]));
+        SmallStore<CF, 6> st;
+        int nn = nact[i], g = 0, s = 0;
+        uint32_t fl = 0u, dr = 0u;
+        bool ok = true;
+        if (nn >= 1) {
+            legal_masks<CF>(P, special_mask<CF, CF::NP>(P), HL, VL, dm);
+            uint32_t act[CF::AW];
+            action_bits<CF>(HL, VL, act, dm);
+            int x = random_action<CF>(act, first);
+            dr = first.draws();
+            for (;;) {
+                if (x < 0) {
+                    fl |= FLAG_NO_LEGAL;
+                    break;
+                }
+                uint32_t f;
+                const int r = apply_action<CF>(P, nn, x, rng, f, HL, VL, st, dm);
+                if (f & FLAG_RECOMPUTE) {
+                    ok = false;
+                    break;
+                }
+                fl |= f;
+                g += r;
+                ++s;
+                --nn;
+                dr = rng.draws();
+                if (nn < 1) break;
+                action_bits<CF>(HL, VL, act, dm);
+                x = random_action<CF>(act, rng);
+                if (rng.overflow) {
+                    ok = false;
+                    break;
+                }
+                dr = rng.draws();
+            }
+        }
+        gain[i] = ok ? g : -1;
+        steps[i] = s;
+        draws[i] = dr;
+        flags[i] = fl;
+    }
+}
+
 using C9 = Cfg<9, 9, 6>;
 using C16 = Cfg<16, 16, 8>;
+// HC_NO_WIDE=1: no 32 x 32-frame instantiations (the MemorySanitizer build: with them its -O0
+// compile needs ~40 GB and most of an hour)
+#ifndef HC_NO_WIDE
+#define HC_NO_WIDE 0
+#endif
 #define M3_F32(b) FCfg<b, 32>
 
 #define DISPATCH(cfg, call)                        \
@@ -322,6 +385,8 @@ using C16 = Cfg<16, 16, 8>;
                 call(FCfg<4>);                     \
             } else if (!wide_) {                   \
                 call(FCfg<5>);                     \
+            } else if (HC_NO_WIDE) {               \
+                abort();                           \
             } else if (bits_ == 2) {               \
                 call(M3_F32(2));                   \
             } else if (bits_ == 3) {               \
@@ -333,6 +398,16 @@ using C16 = Cfg<16, 16, 8>;
             }                                      \
         }                                          \
     } while (0)
+
+// ArrayStore that records whether the scan touched it (get_matches' loop-free path never does)
+template <class CF>
+struct TrapStore : ArrayStore<CF> {
+    bool used = false;
+    bool put(int g, const typename CF::Bd& hh, const typename CF::Bd& vv) {
+        used = true;
+        return ArrayStore<CF>::put(g, hh, vv);
+    }
+};
 
 extern "C" {
 int hc_set_frame(int rows, int columns, int types) {
@@ -386,6 +461,13 @@ int hc_rounds(int cfg, long n, const int8_t* b, const uint32_t* s, const int32_t
 #undef CALL
     return 0;
 }
+int hc_rollout(int cfg, long n, const int8_t* b, const uint32_t* s, const int32_t* na, const uint32_t* rs,
+               int32_t* gain, int32_t* steps, uint32_t* draws, uint32_t* flags) {
+#define CALL(CF) rollout_n<CF>(n, b, s, na, rs, gain, steps, draws, flags)
+    DISPATCH(cfg, CALL);
+#undef CALL
+    return 0;
+}
 long hc_paused(int reset) {
     const long v = g_paused;
     if (reset) g_paused = 0;
@@ -407,6 +489,35 @@ long hc_mask_mismatches(int cfg, long n, const int8_t* b) {
     }
     DISPATCH(cfg, CALL);
 #undef CALL
+    return bad;
+}
+// boards where get_matches (with its loop-free path, M3_FAST_MATCH) differs from the sequential
+// scan in the mask, the spawn planes or the result; *fast counts the boards the loop-free path took
+long hc_fast_match_mismatches(int cfg, long n, const int8_t* b, long* fast) {
+    long bad = 0, nf = 0;
+#define CALL(CF)                                                                           \
+    for (long i = 0; i < n; ++i) {                                                         \
+        using Bd_ = typename CF::Bd;                                                       \
+        Bd_ P[CF::NP], m1, m2, s1[3], s2[3];                                               \
+        const typename CF::Dim dm_ = make_dim<CF>();                                       \
+        load_planes<CF>(b + i * dm_.cells(), P, dm_);                                      \
+        TrapStore<CF>* ts = new TrapStore<CF>;                                             \
+        ArrayStore<CF>* as = new ArrayStore<CF>;                                           \
+        const int r1 = get_matches<CF>(P, m1, s1, *ts);                                    \
+        const int r2 = match_scan<CF, true>(P, m2, s2, *as);                               \
+        nf += r1 == MATCH_FOUND && !ts->used;                                              \
+        delete as;                                                                         \
+        delete ts;                                                                         \
+        bool same = r1 == r2;                                                              \
+        if (r1 == MATCH_FOUND)                                                             \
+            for (int w = 0; w < CF::W; ++w)                                                \
+                same = same && m1.w[w] == m2.w[w] && s1[0].w[w] == s2[0].w[w] &&           \
+                       s1[1].w[w] == s2[1].w[w] && s1[2].w[w] == s2[2].w[w];               \
+        bad += !same;                                                                      \
+    }
+    DISPATCH(cfg, CALL);
+#undef CALL
+    *fast = nf;
     return bad;
 }
 // first n raw outputs via ChainMT2 (the two-block register chain); -1 once it overflowed

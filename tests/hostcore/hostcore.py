@@ -35,6 +35,8 @@ def lib():
         _lib.hc_chain_draw.argtypes = [ctypes.c_uint32, ctypes.c_int]
         _lib.hc_mask_mismatches.restype = ctypes.c_long
         _lib.hc_mask_mismatches.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_void_p]
+        _lib.hc_fast_match_mismatches.restype = ctypes.c_long
+        _lib.hc_fast_match_mismatches.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
     return _lib
 
 
@@ -79,6 +81,14 @@ class HostCore:
         self._sel()
         return lib().hc_mask_mismatches(self.cfg, ctypes.c_long(len(boards)), _p(boards))
 
+    def fast_match_mismatches(self, boards):
+        """(boards where get_matches differs from the sequential scan, boards its loop-free path took)"""
+        boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
+        fast = ctypes.c_long(0)
+        self._sel()
+        bad = lib().hc_fast_match_mismatches(self.cfg, ctypes.c_long(len(boards)), _p(boards), ctypes.byref(fast))
+        return bad, fast.value
+
     def init(self, seeds):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
         n = len(seeds)
@@ -110,6 +120,20 @@ class HostCore:
         lib().hc_roundtrip(self.cfg, ctypes.c_long(len(boards)), _p(boards), _p(out))
         return out
 
+
+    def rollouts(self, boards, seeds, n_actions, rseeds):
+        """rollout_one of k_rollout on the CPU (gain -1: the chain ran out, the kernel's replay case)"""
+        boards = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, self.N)
+        n = len(boards)
+        seeds = np.ascontiguousarray(np.broadcast_to(seeds, (n,)), dtype=np.uint32)
+        na = np.ascontiguousarray(np.broadcast_to(n_actions, (n,)), dtype=np.int32)
+        rs = np.ascontiguousarray(np.broadcast_to(rseeds, (n,)), dtype=np.uint32)
+        gain = np.zeros(n, np.int32); steps = np.zeros(n, np.int32)
+        draws = np.zeros(n, np.uint32); flags = np.zeros(n, np.uint32)
+        self._sel()
+        lib().hc_rollout(self.cfg, ctypes.c_long(n), _p(boards), _p(seeds), _p(na), _p(rs), _p(gain), _p(steps),
+                         _p(draws), _p(flags))
+        return dict(gain=gain, steps=steps, draws=draws, flags=flags)
 
     def init_scalar(self, seeds):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint32)

@@ -132,10 +132,13 @@ def test_rendezvous_server_error_reaches_the_clients():
     from match3tile.rendezvous import Rendezvous, RendezvousServer
 
     srv = RendezvousServer(2, timeout=20)
-    a = Rendezvous(0, 2, srv.address, timeout=20)
+    a = Rendezvous(0, 2, srv.address, server=srv, timeout=20)
     b = Rendezvous(0, 2, srv.address, timeout=20)  # duplicate rank: the server stops
     with pytest.raises(ConnectionError, match="duplicate rank 0"):
         a.allgather(b"x")
+    # the rejected client hears the cause too (its socket gets the error frame, then a clean close)
+    with pytest.raises(ConnectionError, match="duplicate rank 0"):
+        b.allgather(b"y")
     for c in (a, b):
         c.close()
     srv.close()

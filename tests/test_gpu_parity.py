@@ -180,8 +180,9 @@ def test_c3_1m_boards_properties():
 
 @pytest.mark.parametrize("tag", list(SHAPES))
 def test_autoreset_matches_fresh_episodes(tag):
-    """After autoreset, a board continues with seed + stride exactly like a fresh episode
-    (16x16x8: the prefetch resets run entirely on the FullMT pass)."""
+    """After autoreset, a board continues with seed + stride exactly like a fresh episode.
+    (5-move episodes: the second episode's cells come from fill_next_slots' explicit reset; the
+    prefetch path of later episodes is test_autoreset_prefetched_episodes_16x16x8.)"""
     n = 2048
     env = BatchedMatch3Env(n, *SHAPES[tag], num_moves=5, env_goal=BIG, seed_base=100, autoreset=True, seed_stride=n)
     for _ in range(5):
@@ -201,6 +202,38 @@ def test_autoreset_matches_fresh_episodes(tag):
         assert (env.rewards() == fresh.rewards()).all()
         assert (env.observations() == fresh.observations()).all()
     fresh.close()
+    env.close()
+
+
+def test_autoreset_prefetched_episodes_16x16x8():
+    """The step's own prefetch resets, checked on their output: with one-move episodes
+    every step autoresets every board, so steps 4.. swap in episodes that the two-stage 16x16x8 reset
+    (k_reset_stream + k_reset_tiles, the rare sixth-round boards deferred to k_init_coop) built
+    during the run. After each of 10 steps the boards, first actions and seeds must equal an
+    explicit reset of seed_base + b + k * n (k_init_fix_lane), and a sample the oracle's
+    BoardV2.__init__ (boardv2.py:17-27). 8,192 boards: ~33 per episode need the sixth round."""
+    n, base = 8192, 100
+    shape = (16, 16, 8)
+    env = BatchedMatch3Env(n, *shape, num_moves=1, env_goal=BIG, seed_base=base, autoreset=True, seed_stride=n)
+    ctx = _native.Context(*shape)
+    o = Oracle(*shape)
+    pick = np.random.RandomState(5).choice(n, 48, replace=False)
+    for k in range(1, 11):
+        env.step()
+        assert env.dones().all()
+        seeds = np.arange(base + k * n, base + (k + 1) * n, dtype=np.uint32)
+        assert (env.seeds() == seeds).all(), f"step {k}: seeds"
+        want, _, want_first = ctx.init_boards(seeds)
+        obs = env.observations()
+        bad = (obs.reshape(n, -1) != want.reshape(n, -1)).any(1)
+        assert not bad.any(), f"step {k}: {int(bad.sum())} boards differ from a fresh reset (first {np.nonzero(bad)[0][:5]})"
+        assert (env.next_actions() == want_first).all(), f"step {k}: first actions"
+        assert (env.moves() == 0).all() and (env.scores() == 0).all()
+        assert not (env.flags() & _native.FLAG_RESET_CAP).any()
+        for i in pick[(k - 1) * 4:k * 4 + 4]:
+            ob, _ = o.init_board(int(seeds[i]))
+            assert (ob == obs[i]).all(), f"step {k}: board {i} vs the oracle"
+    ctx.close()
     env.close()
 
 

@@ -1,4 +1,10 @@
-"""Register census of the built gfx950 kernels (round 5, DESIGN.md §4 "Lane interference").
+"""Register census and compile flags of the built gfx950 kernels (DESIGN.md §4 "Lane interference").
+
+Round 6 pinned the mechanism: LLVM's SIOptimizeVGPRLiveRange pass. The pre-fix source rebuilt with
+`-mllvm -amdgpu-opt-vgpr-liverange=false` is exact on the frame shapes that failed; the shipped
+library is built with the pass off for every kernel (element-crush-gym_amd/Makefile SAFETY), and
+test_every_code_object_built_with_the_pass_off checks that on the library's own recorded command
+lines (-frecord-command-line), so no kernel reaches the GPU with it on.
 
 The round-4 lane interference needed a kernel that runs several boards per wave AND spills: the
 RNG position carried out of the divergent cascade loop came back stale for the lanes that had left
@@ -19,6 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import spill_audit  # noqa: E402
 
 OBJS = sorted(glob.glob(os.path.join(ROOT, "element-crush-gym_amd", "build", "m3_inst_*.o")))
+LIB = os.path.join(ROOT, "element-crush-gym_amd", "build", "libm3.so")
 REF = os.path.join(ROOT, "profiles", "r05_spill_audit.json")
 pytestmark = pytest.mark.skipif(len(OBJS) < 10, reason="library objects not built (make -C element-crush-gym_amd)")
 
@@ -56,3 +63,16 @@ def test_no_kernel_spills_more_than_committed(census):
              for k, v in census.items()
              if k in ref and v.get("vgpr_spill_count", 0) > ref[k].get("vgpr_spill_count", 0)}
     assert not worse, worse
+
+
+def test_every_code_object_built_with_the_pass_off():
+    """Static check of the shipped artefacts: every gfx950 code object in libm3.so (one per
+    translation unit: the C ABI + 10 configurations) and in each object file was compiled with
+    SIOptimizeVGPRLiveRange off -- the pass behind the lane interference."""
+    dev, host = spill_audit.command_lines(LIB)
+    assert len(dev) >= 11, f"{len(dev)} device command lines recorded in libm3.so (built without -frecord-command-line?)"
+    missing = [x for x in dev + host if spill_audit.SAFETY_FLAG not in x]
+    assert not missing, missing[:2]
+    for obj in OBJS + [os.path.join(ROOT, "element-crush-gym_amd", "build", "m3_api.o")]:
+        d, _ = spill_audit.command_lines(obj)
+        assert d and all(spill_audit.SAFETY_FLAG in x for x in d), obj

@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
-"""Copy a gpu_round.sh run's evidence into profiles/ (tracked) and derive profiles/traffic.json.
+"""Copy a tools/gpu_profile.sh run into profiles/ (tracked) and derive the roofline inputs bench.py reads.
 
-    python3 tools/collect_profiles.py gpurun_out/<tag> <round-tag>
+    python3 tools/collect_profiles.py gpurun_out/<tag>/s9 <round-tag>      (9x9x6 -> profiles/traffic.json)
+    python3 tools/collect_profiles.py gpurun_out/<tag>/s16 <round-tag>     (16x16x8 -> traffic_16x16x8.json)
 
-Writes profiles/<round-tag>_bench.json (the bench line), <round-tag>_kernel_stats.csv
-(rocprofv3 --kernel-trace --stats of the same bench command), <round-tag>_pmc.txt
-(per-kernel PMC means, one rocprofv3 pass per counter group) and traffic.json
-(traffic_<shape>.json for a shape other than 9x9x6):
-HBM bytes per launch of one shard's step pipeline (k_env_step + k_env_cont(_grid) + k_env_fix, the
-two kernels bench.py's HIP events bracket) = 2 * FETCH_SIZE + WRITE_SIZE (KB ->
-bytes), the factor 2 being MI355X_MICROARCH.md's gfx950 correction for wide
-coalesced reads (FETCH_SIZE reports half of them; narrower accesses are
-uncalibrated).
+Every run is the driver's own command (bench.py --gpus 1 --steps 20 --warmup 5 [16x16x8 shape]); the
+kernel trace and each --pmc pass are separate runs of it. Writes:
+  profiles/<rt>[_16x16x8]_bench.json         the bench line of the un-profiled run
+  profiles/<rt>[_16x16x8]_kernel_stats.csv   rocprofv3 --kernel-trace --stats
+  profiles/<rt>[_16x16x8]_dispatch.csv       one row per dispatch of the TIMED window: kernel, every counter
+                                            of every pass (dispatches of one kernel matched across passes
+                                            by their order), and the kernel-trace duration
+  profiles/traffic[_16x16x8].json           per-kernel sums over that window / timed steps, and the
+                                            dominant kernel's (k_env_step) per-launch figures
+Every number in traffic*.json is a sum or ratio of columns of the dispatch CSV (see "how" fields).
+HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes; the factor 2 is MI355X_MICROARCH.md's gfx950
+correction for wide coalesced reads, which FETCH_SIZE reports at half).
 """
 import collections
 import csv
@@ -20,112 +24,147 @@ import json
 import os
 import re
 import shutil
-import subprocess
 import sys
 
-src, tag = sys.argv[1], sys.argv[2]
+src, rtag = sys.argv[1], sys.argv[2]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = os.path.join(ROOT, "profiles")
+KERNELS = ("k_env_step", "k_env_cont_grid", "k_env_fix", "k_init", "k_init_coop", "k_init_fix_lane",
+           "k_reset_stream", "k_reset_tiles")
+VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles
+HBM_PEAK = 8000e9  # B/s
 
 
 def last_json(path):  # (rocprofv3 logs its own lines after the bench line)
     return json.loads([ln for ln in open(path).read().splitlines() if ln.startswith("{")][-1])
 
 
+def kname(name):
+    k = [p for p in KERNELS if re.search(r"\b" + p + "<", name)]
+    return k[0] if k else re.sub(r"\(.*", "", name).replace("void ", "")
+
+
 bench = last_json(os.path.join(src, "bench.log"))
-json.dump(bench, open(os.path.join(P, f"{tag}_bench.json"), "w"), indent=1)
-shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(P, f"{tag}_kernel_stats.csv"))
-pmc = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), src],
-                     capture_output=True, text=True, check=True).stdout
-open(os.path.join(P, f"{tag}_pmc.txt"), "w").write(pmc)
-
-PIPE = ("k_env_step", "k_env_cont", "k_env_cont_grid", "k_env_fix")
-# every kernel that runs inside a timed step: the step pipeline and the autoreset (prefetch) kernels
-STEP_KERNELS = PIPE + ("k_init", "k_init_coop", "k_init_fix_lane", "k_init_chain2", "k_reset_stream", "k_reset_tiles")
-agg = collections.defaultdict(lambda: collections.defaultdict(list))
-# the SQ pass, per dispatch: (dispatch id, kernel, SQ_INSTS_VALU summed over its records)
-disp = collections.defaultdict(lambda: [None, 0.0])
-sq_dir = None
-for f in glob.glob(f"{src}/**/*_counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"]
-        k = [p for p in PIPE if p + "<" in name]
-        if k and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_SALU"):
-            agg[r["Counter_Name"]][k[0]].append(float(r["Counter_Value"]))
-        if r["Counter_Name"] == "SQ_INSTS_VALU":
-            sq_dir = os.path.dirname(os.path.dirname(f))
-            k2 = [p for p in STEP_KERNELS if p + "<" in name]
-            d = disp[int(r["Dispatch_Id"])]
-            d[0] = k2[0] if k2 else re.sub(r"\(.*", "", name).replace("void ", "")
-            d[1] += float(r["Counter_Value"])  # (a counter may come per XCD / SE: summed per dispatch)
+shape = bench["config"]["shape"]
+sfx = "" if shape == "9x9x6" else f"_{shape}"
+json.dump(bench, open(os.path.join(P, f"{rtag}{sfx}_bench.json"), "w"), indent=1)
+shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(P, f"{rtag}{sfx}_kernel_stats.csv"))
 
 
-def per_launch(counter):  # mean per launch of each pipeline kernel, summed over the pipeline
-    return sum(sum(v) / len(v) for v in agg[counter].values())
-
-
-def valu_per_step():
-    """wave64 VALU instructions of one timed step over every kernel it runs, SUMMED over the dispatches
-    of the timed window of the profiled bench command / its timed steps. The window starts at the first
-    dispatch of timed step `warmup` (the (warmup * shards)-th k_env_step) and runs to the last dispatch
-    (nothing is launched after the timed steps). The per-dispatch rows go to profiles/<tag>_valu_dispatch.csv."""
-    sq_log = glob.glob(os.path.join(src, "sq.log"))
-    run = last_json(sq_log[0]) if sq_log else bench  # the bench line of the profiled command itself
-    shards = run["config"].get("shards_per_gpu", 1)
-    warm, steps = run["warmup"], run["steps"]
-    ids = sorted(disp)
-    step_ids = [i for i in ids if disp[i][0] == "k_env_step"]
-    if len(step_ids) < (warm + steps) * shards:
-        raise SystemExit(f"{len(step_ids)} k_env_step dispatches, expected {(warm + steps) * shards}")
-    first = step_ids[-steps * shards]  # the timed steps are the last `steps` of the run
-    per = collections.defaultdict(float)
-    with open(os.path.join(P, f"{tag}_valu_dispatch.csv"), "w") as f:
-        f.write("dispatch_id,kernel,sq_insts_valu,timed\n")
-        for i in ids:
-            k, v = disp[i]
-            timed = i >= first
-            f.write(f"{i},{k},{v:.0f},{int(timed)}\n")
-            if timed and k in STEP_KERNELS:
-                per[k] += v / steps
-    total = sum(per.values())
-    return {"kernels": sorted(per), "per_kernel": dict(per), "share": {k: v / total for k, v in per.items()},
-            "total": total, "shards": shards, "timed_steps": steps, "warmup": warm,
-            "dispatch_csv": f"profiles/{tag}_valu_dispatch.csv",
-            "how": "sum of SQ_INSTS_VALU over every dispatch of the timed window (rocprofv3 --pmc, per-dispatch "
-                   "records) / timed steps"}
-
-
-def duration_share():
-    """each step kernel's share of the kernel-trace duration (rocprofv3 --stats of the same command;
-    the kernels overlap across streams, so these are shares of summed durations, not of wall time)"""
-    rows = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
-    dur = collections.defaultdict(float)
+def dispatches(rows, id_key, name_key):
+    """[(dispatch id, kernel)] in dispatch order"""
+    seen = {}
     for r in rows:
-        k = [p for p in STEP_KERNELS if p + "<" in r["Name"]]
-        if k:
-            dur[k[0]] += float(r["TotalDurationNs"])
-    t = sum(dur.values())
-    return {k: v / t for k, v in dur.items()}
+        seen.setdefault(int(r[id_key]), kname(r[name_key]))
+    return sorted(seen.items())
 
 
-fetch = per_launch("FETCH_SIZE") * 1024
-write = per_launch("WRITE_SIZE") * 1024
-cfg = bench["config"]
-rl = bench["roofline"].get("hbm", bench["roofline"])  # (the HBM block sits inside a VALU-bound roofline)
-traffic = {"shape": cfg["shape"], "boards": cfg["boards_per_gpu"],
-           "kernel": "k_env_step + k_env_cont(_grid) + k_env_fix (the kernels of one shard's step pipeline)",
-           "boards_per_launch": rl.get("boards_per_launch"),
-           "fetch_size_bytes": fetch, "write_size_bytes": write,
-           "hbm_bytes_per_launch": 2 * fetch + write,
-           "bytes_per_board": (2 * fetch + write) / rl.get("boards_per_launch", cfg["boards_per_gpu"]),
-           "valu_insts_per_launch": per_launch("SQ_INSTS_VALU"),
-           "valu_insts_per_step": valu_per_step(),
-           "duration_share": duration_share(),
-           "salu_insts_per_launch": per_launch("SQ_INSTS_SALU"),
-           "source": f"profiles/{tag}_pmc.txt (rocprofv3 --pmc passes: FETCH_SIZE and WRITE_SIZE for the bytes, "
-                     "the SQ_INSTS_VALU / SQ_INSTS_SALU group for the instruction counts)",
-           "correction": "2 x FETCH_SIZE (gfx950 wide-read calibration) + WRITE_SIZE"}
-# one summary per board shape: traffic.json (the headline 9x9x6) / traffic_<shape>.json
-tname = "traffic.json" if cfg["shape"] == "9x9x6" else f"traffic_{cfg['shape']}.json"
+def timed_ids(order, shards, steps):
+    """dispatch ids of the timed window: from the first dispatch of the last `steps` timed steps
+    (the (steps * shards)-th k_env_step from the end) to the last dispatch"""
+    step_ids = [i for i, k in order if k == "k_env_step"]
+    first = step_ids[-steps * shards]
+    return {i for i, _ in order if i >= first}
+
+
+shards, steps, warm = bench["config"]["shards_per_gpu"], bench["steps"], bench["warmup"]
+# per pass: counter values per dispatch, then matched across passes by (kernel, occurrence index)
+table = collections.defaultdict(dict)  # (kernel, occurrence) -> {column: value}
+for f in sorted(glob.glob(os.path.join(src, "p_*", "**", "*_counter_collection.csv"), recursive=True)):
+    rows = list(csv.DictReader(open(f)))
+    order = dispatches(rows, "Dispatch_Id", "Kernel_Name")
+    tids = timed_ids(order, shards, steps)
+    occ, key = collections.Counter(), {}
+    for i, k in order:
+        key[i] = (k, occ[k])
+        occ[k] += 1
+    vals = collections.defaultdict(float)
+    for r in rows:
+        vals[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])  # (summed per dispatch)
+    for (i, c), v in vals.items():
+        if i in tids:
+            table[key[i]][c] = v
+            table[key[i]]["timed"] = 1
+# kernel-trace durations, matched the same way
+kt = list(csv.DictReader(open(glob.glob(os.path.join(src, "kt", "*kernel_trace.csv"))[0])))
+order = sorted({int(r["Dispatch_Id"]): (kname(r["Kernel_Name"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                for r in kt}.items())
+tids = timed_ids([(i, k) for i, (k, _) in order], shards, steps)
+occ = collections.Counter()
+for i, (k, d) in order:
+    if i in tids and (k, occ[k]) in table:
+        table[(k, occ[k])]["duration_ns"] = d
+    occ[k] += 1
+
+cols = sorted({c for v in table.values() for c in v if c != "timed"})
+csv_path = f"profiles/{rtag}{sfx}_dispatch.csv"
+with open(os.path.join(ROOT, csv_path), "w") as f:
+    f.write("kernel,occurrence," + ",".join(cols) + "\n")
+    for (k, n), v in sorted(table.items(), key=lambda kv: (kv[0][0], kv[0][1])):
+        f.write(f"{k},{n}," + ",".join(f"{v.get(c, 0):.0f}" for c in cols) + "\n")
+
+per = collections.defaultdict(lambda: collections.defaultdict(float))
+cnt = collections.Counter()
+for (k, _), v in table.items():
+    cnt[k] += 1
+    for c in cols:
+        per[k][c] += v.get(c, 0.0)
+per_step = {k: {c: x / steps for c, x in d.items()} for k, d in per.items()}
+per_launch = {k: {c: x / cnt[k] for c, x in d.items()} for k, d in per.items()}
+
+d = per_launch["k_env_step"]
+boards_per_launch = -(-bench["config"]["boards_per_gpu"] // shards)
+R, C = (int(x) for x in shape.split("x")[:2])
+alg = 2 * R * C + 21
+hbm = 2 * d.get("FETCH_SIZE", 0) * 1024 + d.get("WRITE_SIZE", 0) * 1024
+simt = d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"])
+ms_step = bench["ms_per_step"]
+valu_step = per_step["k_env_step"]["SQ_INSTS_VALU"]
+dominant = {
+    "kernel": "k_env_step",
+    "launches": cnt["k_env_step"],
+    "boards_per_launch": boards_per_launch,
+    "valu_insts_per_launch": d["SQ_INSTS_VALU"],
+    "valu_insts_per_step": valu_step,
+    "trace_avg_ms": d.get("duration_ns", 0) / 1e6,
+    "valu_frac_trace": d["SQ_INSTS_VALU"] / (d["duration_ns"] / 1e9) / VALU_PEAK,
+    "valu_frac_wall": valu_step / (ms_step / 1e3) / VALU_PEAK,
+    "simt": simt,
+    "lane_frac_wall": valu_step / (ms_step / 1e3) / VALU_PEAK * simt,
+    "hbm_bytes_per_launch": hbm,
+    "hbm_bytes_per_board": hbm / boards_per_launch,
+    "algorithmic_bytes_per_board": alg,
+    "hbm_frac_trace": hbm / (d["duration_ns"] / 1e9) / HBM_PEAK,
+    "wait_frac": d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"],
+    "vmem_wr_per_wave": d["SQ_INSTS_VMEM_WR"] / d["SQ_WAVES"],
+    "vmem_rd_per_wave": d["SQ_INSTS_VMEM_RD"] / d["SQ_WAVES"],
+    "lds_bank_conflict_per_lds_inst": d["SQ_LDS_BANK_CONFLICT"] / max(1.0, d["SQ_INSTS_LDS"]),
+    "bench_ms_per_step": ms_step,
+    "how": {
+        "valu_frac_wall": "valu_insts_per_step (sum of SQ_INSTS_VALU over the timed k_env_step dispatches / steps) "
+                          "/ bench_ms_per_step / VALU peak (256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction)",
+        "valu_frac_trace": "valu_insts_per_launch / trace_avg_ms (the kernel trace's mean duration; the two shards' "
+                           "launches overlap, so this is a per-launch figure, about half the chip's rate)",
+        "simt": "sum SQ_THREAD_CYCLES_VALU / (64 x sum SQ_ACTIVE_INST_VALU) over the timed k_env_step dispatches",
+        "lane_frac_wall": "valu_frac_wall x simt (active lanes' share of the VALU issue peak)",
+        "hbm": "2 x FETCH_SIZE + WRITE_SIZE per launch (KB -> B), gfx950 wide-read correction"},
+}
+pipe = [k for k in ("k_env_step", "k_env_cont_grid", "k_env_fix") if k in per_launch]
+pipe_hbm = sum(2 * per_launch[k].get("FETCH_SIZE", 0) * 1024 + per_launch[k].get("WRITE_SIZE", 0) * 1024 for k in pipe)
+valu_all = {k: v["SQ_INSTS_VALU"] for k, v in per_step.items() if k in KERNELS and "SQ_INSTS_VALU" in v}
+tot = sum(valu_all.values())
+dur = {k: v.get("duration_ns", 0) for k, v in per.items() if k in KERNELS}
+traffic = {
+    "shape": shape, "boards": bench["config"]["boards_per_gpu"], "steps": steps, "warmup": warm,
+    "shards": shards, "boards_per_launch": boards_per_launch,
+    "dominant": dominant,
+    "pipeline": {"kernels": pipe, "hbm_bytes_per_launch": pipe_hbm, "hbm_bytes_per_board": pipe_hbm / boards_per_launch},
+    "valu_insts_per_step": {"per_kernel": valu_all, "total": tot, "share": {k: v / tot for k, v in valu_all.items()},
+                            "how": "sum of SQ_INSTS_VALU over every timed dispatch / steps"},
+    "duration_share": {k: v / sum(dur.values()) for k, v in dur.items()},
+    "dispatch_csv": csv_path,
+    "source": f"gpurun_out pass of tools/gpu_profile.sh -> {csv_path}",
+}
+tname = "traffic.json" if shape == "9x9x6" else f"traffic_{shape}.json"
 json.dump(traffic, open(os.path.join(P, tname), "w"), indent=1)
 print(json.dumps(traffic, indent=1))

@@ -34,5 +34,5 @@ for spec in "$@"; do
   fi
   if [ "${GATED[$L]}" != 0 ]; then echo "$L: REJECTED (parity suite failed, $OUT/parity_$L.log)"; continue; fi
   timeout -k 10 200 python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --check-boards 64 "$@" > $OUT/$i.log 2>&1 || { tail -5 $OUT/$i.log; exit 1; }
-  python3 -c "import json;d=json.loads(open('$OUT/$i.log').read().strip().splitlines()[-1]);print('$L $*: %.4g env-steps/s  %.3f ms/step  kernel %.3f ms  oracle_match %s'%(d['value'],d['ms_per_step'],d['roofline']['hbm']['avg_kernel_ms'],d['parity'].get('oracle_match')))"
+  python3 -c "import json;d=json.loads(open('$OUT/$i.log').read().strip().splitlines()[-1]);r=d['roofline'];print('$L $*: %.4g env-steps/s  %.3f ms/step  k_env_step %.3f ms  pipeline %.3f ms  oracle_match %s'%(d['value'],d['ms_per_step'],r['hbm']['avg_kernel_ms'],r['pipeline']['avg_ms'],d['parity'].get('oracle_match')))"
 done

@@ -62,6 +62,19 @@ def census(objs):
     return out
 
 
+SAFETY_FLAG = "-amdgpu-opt-vgpr-liverange=false"
+
+
+def command_lines(path):
+    """The compile command lines recorded in a library or object (-frecord-command-line, one per
+    code object): (device lines, host lines). Device code objects are the ones built with
+    -mcpu=gfx950; their strings sit uncompressed in the .hip_fatbin bundles."""
+    data = open(path, "rb").read()
+    lines = [m.group(0).decode(errors="replace") for m in re.finditer(rb"/[^\0\n]*/clang-\d+ [^\0\n]*", data)]
+    dev = [x for x in lines if "-mcpu=gfx950" in x]
+    return dev, [x for x in lines if "-mcpu=gfx950" not in x]
+
+
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--") and not a.endswith(".json")]
     objs = args or sorted(glob.glob(os.path.join(ROOT, "element-crush-gym_amd", "build", "m3_inst_*.o")))
