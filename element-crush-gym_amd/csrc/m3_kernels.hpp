@@ -1667,29 +1667,51 @@ __device__ __forceinline__ void env_fin_queue(const EnvArgs& a, int64_t b, uint3
 #endif
 template <class CF>
 __device__ __forceinline__ void coop_reset_cells(const EnvArgs& a, uint64_t m, int64_t ob, uint8_t* lds, int row_stride) {
-    constexpr int NWS = EnvFin<CF>::NWS, PER = 64 / NWS;
+    constexpr int NWS = EnvFin<CF>::NWS;
+    static_assert(NWS <= 64, "one word per lane per board");
+    constexpr int PER = 64 / NWS;             // boards per pass (9x9: 3, 16x16: 1)
+    constexpr int BATCH = PER >= 3 ? 1 : 4;   // passes whose loads go out together
     const int lane = (int)__lane_id(), j = lane / NWS, w = lane - j * NWS;
     while (m) {
-        int src = 0;
-        uint64_t mm = m;
+        uint32_t v[BATCH];
+        int src[BATCH];
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {  // this lane's board of the pass: the j-th set lane of m
-            const int l = mm ? __ffsll((unsigned long long)mm) - 1 : -1;
-            if (k == j) src = l;
-            if (mm) mm &= mm - 1ull;
-        }
-        const int64_t sob = __shfl(ob, src < 0 ? 0 : src);
-        uint32_t v = 0u;
-        if (j < PER && src >= 0) v = a.ne_words[sob * NWS + w];
-        if (j < PER && src >= 0) {
-            uint8_t* dst = lds + src * row_stride + 4 * w;
+        for (int u = 0; u < BATCH; ++u) {
+            src[u] = -1;
 #pragma unroll
-            for (int y = 0; y < 4; ++y)
-                if (4 * w + y < CF::N) dst[y] = (uint8_t)(v >> (8 * y));
+            for (int k = 0; k < PER; ++k) {  // this lane's board of the pass: the j-th set lane of m
+                const int l = m ? __ffsll((unsigned long long)m) - 1 : -1;
+                if (k == j) src[u] = l;
+                if (m) m &= m - 1ull;
+            }
+            const int64_t sob = __shfl(ob, src[u] < 0 ? 0 : src[u]);
+            v[u] = (j < PER && src[u] >= 0) ? a.ne_words[sob * NWS + w] : 0u;
         }
-        m = mm;
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            if (j < PER && src[u] >= 0) {
+                uint8_t* dst = lds + src[u] * row_stride + 4 * w;
+                if constexpr (CF::N % 4 == 0) {
+                    *reinterpret_cast<uint32_t*>(dst) = v[u];  // (rows 16-B aligned: one dword)
+                } else {
+#pragma unroll
+                    for (int y = 0; y < 4; ++y)
+                        if (4 * w + y < CF::N) dst[y] = (uint8_t)(v[u] >> (8 * y));
+                }
+            }
+        }
     }
 }
+
+// k_env_step's extras for the finish of a step: inputs it already holds, and the cooperative copy
+// of the next episode's cells (the wave copies them after the step, coop_reset_cells)
+struct FinOpts {
+    const uint32_t* slot = nullptr;  // the board's current episode slot (else loaded again)
+    const uint32_t* seed = nullptr;  // the board's seed (else loaded again)
+    bool cells = true;               // false: leave the next episode's cells to coop_reset_cells
+    bool* reset = nullptr;           // out: this lane swapped in its next episode
+    int64_t* ob = nullptr;           // out: that episode's slot word offset
+};
 
 // rank of this lane among the set lanes of m
 __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
@@ -1699,9 +1721,12 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
 template <class CF, class RNG, class Store>
 __device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
                                            int r, uint32_t f, const typename CF::Bd& HL, const typename CF::Bd& VL,
-                                           int mv, int sc0, const typename CF::Dim& dm, uint8_t* row = nullptr) {
+                                           int mv, int sc0, const typename CF::Dim& dm, uint8_t* row = nullptr,
+                                           FinOpts o = FinOpts{}) {
     EnvFin<CF> e;
-    if (!env_fin_begin<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm, row, e)) return false;
+    if (!env_fin_begin<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm, row, e, o.slot, o.seed, o.cells)) return false;
+    if (o.reset) *o.reset = e.reset;
+    if (o.ob) *o.ob = e.ob;
     // the freed slot is queued for the episode after next: one atomic per wave, not per lane
     const uint64_t m = __ballot(e.reset);
     uint32_t qbase = 0u;
@@ -1712,7 +1737,7 @@ __device__ __forceinline__ bool env_finish(typename CF::Bd* P, const EnvArgs& a,
     }
     prof_drain(st);
     mark<PH_TATOM>(st);
-    env_fin_store<CF>(P, a, b, st, e, dm, row);
+    env_fin_store<CF>(P, a, b, st, e, dm, row, o.cells);
     if (m) {
         qbase = __shfl(qbase, leader);
         if (e.reset) env_fin_queue(a, b, qbase + lane_rank(m), e.seed, e.s_old);
@@ -1735,7 +1760,7 @@ constexpr uint32_t FLAG_CONT_DEAD = 0x80u;
 template <class CF, bool DEFER, class RNG, class Store>
 __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a, int64_t b, RNG& rng, Store& st,
                                             int limit, int& r, uint32_t& f, const typename CF::Dim& dm,
-                                            uint8_t* row = nullptr) {
+                                            uint8_t* row = nullptr, FinOpts o = FinOpts{}) {
     // every per-board input is loaded before the cascade, so its latency hides behind it
     const int act_in = a.actions ? a.actions[b] : a.next_action[b];
     const int mv = a.moves[b];
@@ -1752,8 +1777,8 @@ __device__ __forceinline__ int env_step_one(typename CF::Bd* P, const EnvArgs& a
         }
     }
     if (f & FLAG_RECOMPUTE) return ENV_STEP_RECOMPUTE;
-    return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm, row) ? ENV_STEP_DONE
-                                                                                   : ENV_STEP_RECOMPUTE;
+    return env_finish<CF>(P, a, b, rng, st, r, f, HL, VL, mv, sc0, dm, row, o) ? ENV_STEP_DONE
+                                                                                      : ENV_STEP_RECOMPUTE;
 }
 
 // Continuation records of paused steps (KS::CASCADE_LIMIT): word 0 the
@@ -1914,14 +1939,23 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
             }
             mark<PH_QUEUE>(st);
         } else {
-            res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f, dm, row);
+            FinOpts o;
+            const uint32_t seed_in = rng.seed;
+            if constexpr (!CF::DYN) {
+                o.slot = &cslot;
+                o.seed = &seed_in;
+                o.cells = !M3_COOP_CELLS;
+                o.reset = &reset_lane;
+                o.ob = &reset_ob;
+            }
+            res = env_step_one<CF, false>(P, a, b, rng, st, -1, r, f, dm, row, o);
             if (res == ENV_STEP_RECOMPUTE) {  // (its row is rewritten by k_env_fix)
                 const uint32_t slot = atomicAdd(&a.counters[CNT_OVF], 1u);
                 a.ovf_list[slot] = (uint32_t)b;
             }
         }
     }
-    if constexpr (K::CASCADE_LIMIT >= 0 && M3_COOP_CELLS && !CF::DYN) {
+    if constexpr (M3_COOP_CELLS && !CF::DYN) {
         const uint64_t mr = __ballot(reset_lane);  // (all 64 lanes: a ragged last wave too)
         if (mr) coop_reset_cells<CF>(a, mr, reset_ob, lds, NC + RPAD);
     }

@@ -44,3 +44,21 @@ def test_hostcore_rule_code_under_asan_ubsan():
     assert r.returncode == 0, out[-4000:]
     _clean(out)
     assert "no sanitizer report" in out
+
+
+HC_MSAN = os.path.join(HC, "build", "hostcore_msan")
+
+
+def test_hostcore_rule_code_under_msan():
+    """MemorySanitizer over the same harness (round 6: ruling out an uninitialised read behind the
+    lane interference): every hostcore entry point incl. rollouts on the headline and
+    16 x 16-frame shapes, HC_N boards per shape (the instrumented -O0 build is slow; the committed
+    run is profiles/r06_hostcore_msan.log). Built by `make -C tests/hostcore msan` (~30 min)."""
+    if not os.path.exists(HC_MSAN):
+        pytest.skip("MemorySanitizer hostcore not built (make -C tests/hostcore msan, ~30 min)")
+    env = dict(os.environ, HC_N=os.environ.get("HC_N", "4"), MSAN_OPTIONS="halt_on_error=0")
+    r = subprocess.run([HC_MSAN], capture_output=True, text=True, timeout=3000, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "MemorySanitizer" not in out, out[-4000:]
+    assert "no sanitizer report" in out

@@ -10,7 +10,7 @@ The round-4 lane interference needed a kernel that runs several boards per wave 
 RNG position carried out of the divergent cascade loop came back stale for the lanes that had left
 the loop early. The frame kernels now run that loop wave-uniform; this census keeps the 16 x 16
 frame's board-per-lane step kernels out of scratch (at most a few values spilled to AGPRs) and holds every kernel to the spill counts
-committed in profiles/r05_spill_audit.json (a ratchet: a build that spills more fails here, on the
+committed in profiles/r06_spill_audit.json (a ratchet: a build that spills more fails here, on the
 CPU, before any GPU run). Reads the code-object metadata of build/m3_inst_*.o (tools/spill_audit.py).
 """
 import glob
@@ -26,7 +26,7 @@ import spill_audit  # noqa: E402
 
 OBJS = sorted(glob.glob(os.path.join(ROOT, "element-crush-gym_amd", "build", "m3_inst_*.o")))
 LIB = os.path.join(ROOT, "element-crush-gym_amd", "build", "libm3.so")
-REF = os.path.join(ROOT, "profiles", "r05_spill_audit.json")
+REF = os.path.join(ROOT, "profiles", "r06_spill_audit.json")
 pytestmark = pytest.mark.skipif(len(OBJS) < 10, reason="library objects not built (make -C element-crush-gym_amd)")
 
 # board-per-lane kernels of the 16 x 16 frame that must keep every value in registers (a few spill
