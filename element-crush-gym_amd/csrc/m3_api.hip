@@ -755,8 +755,15 @@ int m3_env_set_shards(m3_env* e, int nshards) {
         m3_env::Shard sh;
         sh.off = std::min<int64_t>(e->n, s * per);
         sh.n = std::min<int64_t>(e->n, sh.off + per) - sh.off;
-        HIP_TRY(hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&sh.pstream, hipStreamNonBlocking));
+        if (M3_STREAM_PRIO) {  // the step stream first at dispatch, the prefetch resets last
+            int least = 0, greatest = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIP_TRY(hipStreamCreateWithPriority(&sh.stream, hipStreamNonBlocking, greatest));
+            HIP_TRY(hipStreamCreateWithPriority(&sh.pstream, hipStreamNonBlocking, least));
+        } else {
+            HIP_TRY(hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking));
+            HIP_TRY(hipStreamCreateWithFlags(&sh.pstream, hipStreamNonBlocking));
+        }
         HIP_TRY(hipEventCreateWithFlags(&sh.ev, hipEventDisableTiming));
         for (hipEvent_t& ev : sh.pev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         for (hipEvent_t& ev : sh.aev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));

@@ -142,6 +142,15 @@ struct KS {
     // the 3-waves/SIMD bound shifts with it.
     using Chain = std::conditional_t<(CF::N > 128), ChainMT1, ChainMT>;
     using Rng = Chain;
+// Issue priorities against the prefetch resets that share the SIMDs (A/B knobs, off by default):
+// M3_STEP_PRIO -- s_setprio of the k_env_step waves; M3_STREAM_PRIO -- the shard's step stream at
+// the device's greatest stream priority and its prefetch stream at the least.
+#ifndef M3_STEP_PRIO
+#define M3_STEP_PRIO 0
+#endif
+#ifndef M3_STREAM_PRIO
+#define M3_STREAM_PRIO 0
+#endif
 #ifndef M3_CASCADE_LIMIT
 #define M3_CASCADE_LIMIT 2
 #endif
@@ -1831,6 +1840,7 @@ __global__ void __launch_bounds__(KS<CF>::B, KS<CF>::STEP_WPS) k_env_step(EnvArg
     // inside it; with one wave per workgroup nothing else can touch the LDS
     // in between, so the two share storage (9 KB per wave at 9x9: the 6-slot table).
     using K = KS<CF>;
+    if constexpr (M3_STEP_PRIO > 0) __builtin_amdgcn_s_setprio(M3_STEP_PRIO);
     static_assert(K::B == 64, "staging/table aliasing assumes one wave per workgroup");
     // 16x16: staging rows padded by 16 B (block_copy_in_rows)
     constexpr int RPAD = (!CF::DYN && CF::N % 64 == 0 && M3_STAGE_PAD) ? 16 : 0;
