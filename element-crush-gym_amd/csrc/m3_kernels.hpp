@@ -72,6 +72,21 @@ constexpr int MAX_SHARDS = 8;  // env board shards (one HIP stream each)
 #endif
 constexpr uint32_t RESET_KCAP = M3_RESET_KCAP;
 // grid caps of the env-prefetch reset kernels (0: sized by the queue's usual length), see launch_init
+// The prefetch reset launches are sized for n / PF_DIV queued resets of the shard (grid-strided beyond
+// that; blocks past the queue's length exit at once). Round 6: every board's episode ends on the same
+// step (the bench's 20-move episodes all start together), so one step in 20 queues the whole shard;
+// sized for n / 8 (round 5) that burst ran ~1 wave per SIMD for 1.3-1.8 ms and held the step that
+// reuses the queue ~1 ms. A/B (driver command): 9x9 n / 1 2.53-2.55 vs 2.41-2.42 G env-steps/s,
+// 16x16 n / 2 0.79-0.80 vs 0.78 (n / 1 0.76-0.79). Frame shapes keep n / 8.
+#ifndef M3_PF_DIV
+#define M3_PF_DIV 1
+#endif
+#ifndef M3_PF_DIV16
+#define M3_PF_DIV16 2
+#endif
+#ifndef M3_COOP_GMAX  // most blocks of a prefetch k_init_coop launch (one deferred reset per wave at a time)
+#define M3_COOP_GMAX 4096
+#endif
 #ifndef M3_PF_GRID
 #define M3_PF_GRID 0
 #endif
@@ -612,13 +627,20 @@ __global__ void __launch_bounds__(FIX_BLOCK) k_apply_fix(ApplyArgs a) {
     }
 }
 
-constexpr int NSLOT = 4;            // episode slots per board (see EnvArgs)
+// M3_NSLOT: episode slots per board (A/B knob; at most 5: the counter blocks below). Round 6 A/B
+// of 5 slots -- one more step of slack for the synchronised end-of-episode reset bursts: equal speed.
+#ifndef M3_NSLOT
+#define M3_NSLOT 4
+#endif
+constexpr int NSLOT = M3_NSLOT;     // episode slots per board (see EnvArgs)
+static_assert(NSLOT >= 2 && NSLOT <= 255, "slot index is a byte");
 constexpr int PF_LAG = NSLOT - 1;   // steps between a prefetch and its first use
 // Per-shard counter blocks (8 words each), by step % CBLOCKS. Step t's block is read last by its
 // prefetch chain, which step t + PF_LAG waits for; so when step t + PF_LAG's k_env_fix runs, the
 // block of step t + PF_LAG + 1 (= step t's) is free and that kernel zeroes it -- no fill dispatch
 // per shard-step and no cross-block ticket.
 constexpr int CBLOCKS = PF_LAG + 1;
+static_assert(8 * CBLOCKS <= 40, "the counter blocks end where a shard's stats begin (m3_env::counters, word 40)");
 #ifndef M3_STAGE_PAD  // k_env_step's 16x16 staging rows 16 B apart (bank conflicts, see block_copy_in_rows)
 #define M3_STAGE_PAD 1
 #endif
@@ -2391,7 +2413,7 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
         if (a.defer) {  // sized for the usual ~4 % deferred share, grid-strided
             HIP_TRY(hipGetLastError());
             int64_t gc = max_items / 16 + 1;
-            gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+            gc = gc < 64 ? 64 : (gc > M3_COOP_GMAX ? M3_COOP_GMAX : gc);
             if (coop_cap > 0 && gc > coop_cap) gc = coop_cap;
             hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
         }
@@ -2414,7 +2436,7 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
             hipLaunchKernelGGL(k_reset_tiles<CF>, dim3((unsigned)(g > 4096 ? 4096 : g)), dim3(64), 0, stream, s);
             HIP_TRY(hipGetLastError());
             int64_t gc = max_items / 32 + 1;  // the ~2 % past the table's rounds
-            gc = gc < 64 ? 64 : (gc > 4096 ? 4096 : gc);
+            gc = gc < 64 ? 64 : (gc > M3_COOP_GMAX ? M3_COOP_GMAX : gc);
             if (coop_cap > 0 && gc > coop_cap) gc = coop_cap;
             hipLaunchKernelGGL(k_init_coop<CF>, dim3((unsigned)gc), dim3(64), 0, stream, a);
         }
@@ -2549,9 +2571,10 @@ int launch_env_shard(m3_env* e, int s, const int32_t* d_actions) {
             r.defer_count = &cnt[CNT_PF_DEFER];  // zeroed with the block
         }
         prefetch_args<CF>(e, o, r);
-        // the grid is sized for the expected number of finished boards and grid-strides
+        // the grid is sized for n / PF_DIV finished boards and grid-strides (M3_PF_DIV)
 #ifndef M3_DEBUG_NO_PREFETCH  // timing experiment only: the next episodes are never built (not bit-exact)
-        int rc = launch_init<CF>(sh.pstream, r, sh.n / 8 + 1);
+        constexpr int64_t PF_DIV = CF::DYN ? 8 : (CF::N > 128 ? M3_PF_DIV16 : M3_PF_DIV);
+        int rc = launch_init<CF>(sh.pstream, r, sh.n / PF_DIV + 1);
         if (rc) return rc;
 #endif
         HIP_TRY(hipEventRecord(sh.pev[par], sh.pstream));
