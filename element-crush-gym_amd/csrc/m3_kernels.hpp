@@ -906,7 +906,7 @@ __device__ uint32_t wave_reset(const InitArgs& a, int64_t item, uint32_t* key, u
 // right away (wave_reset).
 // REDO: the explicit-reset form, whose wave redoes its >= 624-draw resets itself (wave_reset, 2.5 KB
 // of LDS for the MT state); the env prefetch (a.defer) defers them to k_init_coop instead and leaves
-// that LDS out, so with the tile ring its wave takes ~14 KB -- what a CU full of k_env_step waves
+// that LDS out, so with the 10-word tile ring its wave takes ~10 KB -- what a CU full of k_env_step waves
 // (16 x 9 KB) still has free.
 template <class CF, bool REDO>
 __global__ void __launch_bounds__(INIT_BLOCK) k_init(InitArgs a) {
@@ -2387,7 +2387,7 @@ int launch_init(hipStream_t stream, const InitArgs& a, int64_t max_items) {
     int64_t g = (max_items + INIT_BLOCK - 1) / INIT_BLOCK;
     if (g > 4096) g = 4096;
     // env prefetch (a.defer): the reset kernels grid-stride over the queue, and their waves share the
-    // CUs with the step kernels (k_init holds 21.5 KB of LDS per wave, two and a half step waves'
+    // CUs with the step kernels (k_init holds ~10 KB of LDS per wave, about one step wave's
     // worth); capping their grids bounds how many run at once. The queue is needed PF_LAG steps later.
     const int64_t pf_cap = a.defer ? (int64_t)M3_PF_GRID : 0, coop_cap = a.defer ? (int64_t)M3_PF_COOP_GRID : 0;
     if (pf_cap > 0 && g > pf_cap) g = pf_cap;

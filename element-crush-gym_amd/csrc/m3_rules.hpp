@@ -1508,12 +1508,23 @@ M3_HD void init_board(typename CF::Bd* P, RNG& mt, S& st, const typename CF::Dim
 // a lane's unread tiles span about N + one 64-draw chunk + the acceptance spread between lanes (9x9:
 // ~150-250 tiles of the 16-word ring's 384 usable). A lane whose unread tiles would overrun the ring
 // stops (its reset reports the cap: the exact fallback redoes it), so the ring never loses a tile.
-// At 9x9 this halves k_init's LDS (tm: 16 KB -> 12 KB per wave).
+// 9x9: 10 words per plane (192 usable tiles; indexed modulo 10): tm 7.5 KB + pos 2.3 KB per wave,
+// so more reset waves fit a CU beside the step waves (k_init is LDS-bound). A/B on the driver
+// command: 16 words 2.50-2.51, 12 2.53-2.57, 10 2.60, 8 2.25-2.29 G env-steps/s (too small: resets
+// overrun the ring and go to the wave-per-board fallback).
 template <class CF>
 struct TileGen {
-    static constexpr int TWMAX = CF::N <= 128 ? 16 : 32;  // ring words per plane (a power of two)
-    static constexpr int MAXR = 624 / CF::N + 2;         // rounds one MT block can feed
-    static_assert((TWMAX & (TWMAX - 1)) == 0, "ring index by mask");
+#ifndef M3_TW9
+#define M3_TW9 10
+#endif
+    static constexpr int TWMAX = CF::N <= 128 ? M3_TW9 : 32;  // ring words per plane
+    static constexpr int MAXR = 624 / CF::N + 2;             // rounds one MT block can feed
+    static_assert(TWMAX > CF::W + 1, "a round's read window fits the ring");
+    // ring slot of stream word q (a mask for a power of two, else a modulo by a constant)
+    static M3_HD uint32_t slot(uint32_t q) {
+        if constexpr ((TWMAX & (TWMAX - 1)) == 0) return q & (uint32_t)(TWMAX - 1);
+        else return q % (uint32_t)TWMAX;
+    }
 };
 
 
@@ -1560,7 +1571,7 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
                 if ((nt & 31u) == 0u) {
 #pragma unroll
                     for (int p = 0; p < CF::BITS; ++p) {
-                        tm[(p * TW + (int)(((nt >> 5) - 1u) & (uint32_t)(TW - 1))) * stride] = cur[p];
+                        tm[(p * TW + (int)TileGen<CF>::slot((nt >> 5) - 1u)) * stride] = cur[p];
                         cur[p] = 0u;
                     }
                 }
@@ -1569,7 +1580,7 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
         }
 #pragma unroll
         for (int p = 0; p < CF::BITS; ++p)  // the partial word, so a round can read it
-            tm[(p * TW + (int)((nt >> 5) & (uint32_t)(TW - 1))) * stride] = cur[p];
+            tm[(p * TW + (int)TileGen<CF>::slot(nt >> 5)) * stride] = cur[p];
     };
     // make sure every lane that still needs them has `need` tiles (or the block is exhausted)
     auto ensure = [&](uint32_t need, bool want) {
@@ -1584,10 +1595,10 @@ M3_HD bool init_board_tiles(typename CF::Bd* P, RNG& g, uint32_t* tm, uint32_t* 
         const uint32_t sh = j & 31u;
 #pragma unroll
         for (int p = 0; p < CF::BITS; ++p) {
-            uint32_t lo = tm[(p * TW + (int)(q & (uint32_t)(TW - 1))) * stride];
+            uint32_t lo = tm[(p * TW + (int)TileGen<CF>::slot(q)) * stride];
 #pragma unroll
             for (int i = 0; i < CF::W; ++i) {
-                const uint32_t hi = tm[(p * TW + (int)((q + (uint32_t)i + 1u) & (uint32_t)(TW - 1))) * stride];
+                const uint32_t hi = tm[(p * TW + (int)TileGen<CF>::slot(q + (uint32_t)i + 1u)) * stride];
                 T[p].w[i] = sh ? ((lo >> sh) | (hi << (32u - sh))) : lo;
                 lo = hi;
             }
