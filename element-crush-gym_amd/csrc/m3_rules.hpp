@@ -1506,7 +1506,7 @@ M3_HD void init_board(typename CF::Bd* P, RNG& mt, S& st, const typename CF::Dim
 // The stream is kept as a RING of TWMAX plane words (round 6; was the whole 624-tile stream, 21
 // words): a round only reads its own N tiles, and every live lane of a wave is at the same round, so
 // a lane's unread tiles span about N + one 64-draw chunk + the acceptance spread between lanes (9x9:
-// ~150-250 tiles of the 16-word ring's 384 usable). A lane whose unread tiles would overrun the ring
+// 192 usable tiles in the 10-word ring below are enough for all but a few). A lane whose unread tiles would overrun the ring
 // stops (its reset reports the cap: the exact fallback redoes it), so the ring never loses a tile.
 // 9x9: 10 words per plane (192 usable tiles; indexed modulo 10): tm 7.5 KB + pos 2.3 KB per wave,
 // so more reset waves fit a CU beside the step waves (k_init is LDS-bound). A/B on the driver
